@@ -1,0 +1,44 @@
+# Build of the MI355X path-tracing hot path.
+#   librtpt.so   gfx950 HIP kernel + C-ABI (include/rtpt.h)     -> gpuraytracer_amd/
+#   rtrace       C++ CLI host (mirrors RTrace/main.swift)       -> gpuraytracer_amd/
+#   oracle       CPU oracle for tests / cpu_baseline            -> oracle/liboracle.so
+# Every TU is compiled with -ffp-contract=off: the arithmetic contract of
+# DESIGN.md §3 (explicit fmaf only) that makes GPU == oracle bit-exact.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := gpuraytracer_amd
+SRC := $(PKG)/csrc
+BLD := build
+COMMON := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude
+HOSTCXX ?= /opt/rocm/llvm/bin/clang++
+HIPFLAGS := $(COMMON) --offload-arch=$(ARCH)
+HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include
+
+OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
+HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp
+
+all: $(PKG)/librtpt.so $(PKG)/rtrace oracle
+
+$(BLD):
+	mkdir -p $(BLD)
+
+$(BLD)/rt_kernel.o: $(SRC)/rt_kernel.hip $(HDRS) | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BLD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BLD)
+	$(HOSTCXX) $(HOSTFLAGS) -c $< -o $@
+
+$(PKG)/librtpt.so: $(OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -Wl,--no-undefined
+
+$(PKG)/rtrace: $(SRC)/rtrace_main.cpp $(PKG)/librtpt.so $(HDRS)
+	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lrtpt -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BLD) $(PKG)/librtpt.so $(PKG)/rtrace
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

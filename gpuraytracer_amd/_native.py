@@ -1,0 +1,172 @@
+"""ctypes binding of librtpt.so (the C-ABI declared in include/rtpt.h).
+
+The ABI structs mirror ``RTrace/shaderTypes.h`` (see include/rt_types.h):
+Apple ``simd_float3`` is 16 bytes with 16-byte alignment, so the padding that
+the C compiler inserts is spelled out explicitly here and every size is
+asserted against the C header's static asserts.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+ABI_VERSION = 1
+_HERE = os.path.dirname(os.path.abspath(__file__))
+library_path = os.path.join(_HERE, "librtpt.so")
+
+
+class float3(ctypes.Structure):
+    """simd_float3: x, y, z + 4 bytes of padding (16 B)."""
+
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float),
+                ("_pad", ctypes.c_float)]
+
+    def __iter__(self):
+        return iter((self.x, self.y, self.z))
+
+
+class float4(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float),
+                ("w", ctypes.c_float)]
+
+
+class int2(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32)]
+
+
+class MaterialGPU(ctypes.Structure):  # shaderTypes.h:13-18
+    _fields_ = [("diffuse", float4), ("metallic", ctypes.c_float),
+                ("roughness", ctypes.c_float), ("_pad", ctypes.c_float * 2),
+                ("emissive", float3)]
+
+
+class SphereGPU(ctypes.Structure):  # shaderTypes.h:25-29
+    _fields_ = [("center", float3), ("material", MaterialGPU), ("radius", ctypes.c_float),
+                ("_pad", ctypes.c_float * 3)]
+
+
+class CameraGPU(ctypes.Structure):  # shaderTypes.h:31-38
+    _fields_ = [("position", float3), ("direction", float3), ("up", float3),
+                ("resolution", int2), ("horizontalFov", ctypes.c_float),
+                ("ev100", ctypes.c_float)]
+
+
+class SquareLightGPU(ctypes.Structure):  # shaderTypes.h:56-62
+    _fields_ = [("center", float3), ("color", float4), ("emittedRadiance", float3),
+                ("width", ctypes.c_float), ("depth", ctypes.c_float),
+                ("_pad", ctypes.c_float * 2)]
+
+
+for _t, _n in ((float3, 16), (MaterialGPU, 48), (SphereGPU, 80), (CameraGPU, 64),
+               (SquareLightGPU, 64)):
+    assert ctypes.sizeof(_t) == _n, (_t.__name__, ctypes.sizeof(_t))
+assert MaterialGPU.emissive.offset == 32 and SphereGPU.radius.offset == 64
+assert CameraGPU.resolution.offset == 48 and CameraGPU.horizontalFov.offset == 56
+assert SquareLightGPU.width.offset == 48
+
+
+class SceneDesc(ctypes.Structure):  # rt_scene_desc
+    _fields_ = [("camera", ctypes.POINTER(CameraGPU)),
+                ("materials", ctypes.POINTER(MaterialGPU)),
+                ("square_lights", ctypes.POINTER(SquareLightGPU)),
+                ("n_square_lights", ctypes.c_uint32),
+                ("vertices", ctypes.POINTER(float3)),
+                ("n_triangles", ctypes.c_uint32),
+                ("spheres", ctypes.POINTER(SphereGPU)),
+                ("n_spheres", ctypes.c_uint32),
+                ("device", ctypes.c_int32)]
+
+
+class RenderParamsC(ctypes.Structure):  # rt_render_params
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                ("spp", "bounces", "sample_base", "row_start", "row_step", "row_count",
+                 "accumulate", "flags")]
+
+
+RT_OK = 0
+RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE, RT_KEEP_SUM = 0x1, 0x2, 0x4, 0x8
+RT_MAX_BOUNCES = 4
+STATUS = {0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_NO_DEVICE", 3: "RT_ERR_OUT_OF_MEMORY",
+          4: "RT_ERR_LAUNCH", 5: "RT_ERR_STATE", 6: "RT_ERR_COMM"}
+
+# Every entry point of include/rtpt.h: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+SIGNATURES = {
+    "rt_create": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(_P)]),
+    "rt_set_seeds": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32]),
+    "rt_fill_seeds": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "rt_render": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P]),
+    "rt_render_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),
+    "rt_last_kernel_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
+    "rt_destroy": (ctypes.c_int, [_P]),
+    "rt_last_error": (ctypes.c_char_p, [_P]),
+    "rt_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "rt_abi_version": (ctypes.c_int, []),
+    "rt_seed_splitmix": (None, [ctypes.c_uint64, _P, ctypes.c_size_t]),
+    "rt_scene_cornell_box": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.POINTER(CameraGPU),
+                                            ctypes.POINTER(MaterialGPU),
+                                            ctypes.POINTER(float3),
+                                            ctypes.POINTER(SquareLightGPU),
+                                            ctypes.POINTER(ctypes.c_uint32)]),
+    "rt_scene_random_spheres": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                                               ctypes.c_uint64, ctypes.POINTER(CameraGPU),
+                                               ctypes.POINTER(MaterialGPU),
+                                               ctypes.POINTER(float3),
+                                               ctypes.POINTER(SquareLightGPU),
+                                               ctypes.POINTER(ctypes.c_uint32),
+                                               ctypes.POINTER(SphereGPU)]),
+    "rt_tonemap_rgba8": (None, [_P, ctypes.c_size_t, _P]),
+}
+
+
+class RtError(RuntimeError):
+    """A non-RT_OK status from librtpt.so, with rt_last_error()'s message."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS.get(status, status)}: {message}")
+        self.status = status
+
+
+def _preload_hip_runtime():
+    """Make this process use ONE HIP runtime.
+
+    torch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7, NEEDED as
+    "libamdhip64.so").  If librtpt.so pulled in /opt/rocm's copy first, torch
+    would later map a second runtime and fail to see the GPU ("No HIP GPUs are
+    available").  Preloading torch's copy (without importing torch) makes
+    librtpt.so's NEEDED libamdhip64.so.7 resolve to it and torch reuse it, so
+    device pointers, streams and events are shared.  Without torch the system
+    runtime is used.  RTPT_SYSTEM_HIP=1 opts out.
+    """
+    if os.environ.get("RTPT_SYSTEM_HIP") == "1":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        cand = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
+def _load():
+    if not os.path.exists(library_path):
+        raise ImportError(
+            f"{library_path} is missing: build the HIP extension first "
+            "(`make` or `python -c 'import __graft_entry__ as g; g.build()'`). "
+            "There is no CPU fallback.")
+    _preload_hip_runtime()
+    handle = ctypes.CDLL(library_path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if handle.rt_abi_version() != ABI_VERSION:
+        raise ImportError(f"librtpt.so ABI {handle.rt_abi_version()} != {ABI_VERSION}")
+    return handle
+
+
+lib = _load()

@@ -1,0 +1,392 @@
+// rt_api.cpp — the C-ABI of librtpt.so (include/rtpt.h).
+//
+// Replaces the Metal host boundary of the reference:
+//   Renderer.init()  (RTrace/renderer.swift:29-115)  -> rt_create / rt_set_seeds
+//   Renderer.draw()  (RTrace/renderer.swift:117-146) -> rt_render
+// Inputs are copied at create time (makeBuffer(bytes:) semantics), the context
+// owns every device buffer, and every failure is returned as an rt_status with
+// a message (the reference fatalError()s / force-unwraps instead).
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "../../include/rtpt.h"
+#include "rt_kernel.hpp"
+#include "rt_scene.hpp"
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    rt::CompiledScene scene;
+    float4* d_tri_isect = nullptr;
+    float4* d_tri_shade = nullptr;
+    float4* d_sph_isect = nullptr;
+    float4* d_sph_shade = nullptr;
+    uint32_t* d_seeds = nullptr;
+    bool seeds_ready = false;
+    float4* d_sum = nullptr;
+    size_t sum_cap = 0;  // pixels
+    bool sum_valid = false;
+    uint32_t sum_row_start = 0, sum_row_step = 0, sum_row_count = 0, sum_samples = 0;
+    void* d_out = nullptr;  // staging for host outputs
+    size_t out_cap = 0;     // bytes
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_err = "no error";
+
+int fail(rt_ctx* ctx, int status, const std::string& msg) {
+    if (ctx)
+        ctx->err = msg;
+    else
+        g_create_err = msg;
+    return status;
+}
+
+int hip_fail(rt_ctx* ctx, int status, const char* what, hipError_t e) {
+    return fail(ctx, status, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Makes ctx->device current for the duration of an API call, restores after.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+hipError_t upload(T** dptr, const void* src, size_t bytes, hipStream_t s) {
+    *dptr = nullptr;
+    if (bytes == 0) return hipSuccess;
+    hipError_t e = hipMalloc((void**)dptr, bytes);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(*dptr, src, bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+void release(rt_ctx* c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    (void)hipFree(c->d_tri_isect);
+    (void)hipFree(c->d_tri_shade);
+    (void)hipFree(c->d_sph_isect);
+    (void)hipFree(c->d_sph_shade);
+    (void)hipFree(c->d_seeds);
+    (void)hipFree(c->d_sum);
+    (void)hipFree(c->d_out);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// Resolves row partition defaults and validates it against the frame height.
+bool resolve_rows(const rt_ctx* c, const rt_render_params* p, uint32_t* start, uint32_t* step,
+                  uint32_t* count) {
+    const uint32_t H = (uint32_t)c->scene.cam.H;
+    *start = p->row_start;
+    *step = p->row_step ? p->row_step : 1u;
+    if (*start >= H) return false;
+    const uint32_t avail = (H - 1u - *start) / *step + 1u;
+    *count = p->row_count ? p->row_count : avail;
+    return *count <= avail;
+}
+
+int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_device,
+                hipStream_t stream, bool sync) {
+    if (!p) return fail(c, RT_ERR_INVALID_ARG, "params is null");
+    if (p->bounces > RT_MAX_BOUNCES)
+        return fail(c, RT_ERR_INVALID_ARG,
+                    "bounces > 4: Halton dimensions would leave primes[24] (sampling.metal:97)");
+    if (!c->seeds_ready) return fail(c, RT_ERR_STATE, "seeds not set (rt_set_seeds/rt_fill_seeds)");
+    uint32_t start, step, count;
+    if (!resolve_rows(c, p, &start, &step, &count))
+        return fail(c, RT_ERR_INVALID_ARG, "row partition outside the frame");
+    const bool want_out = !(p->flags & RT_OUT_NONE);
+    const bool keep_sum = (p->flags & RT_KEEP_SUM) != 0;
+    if (want_out && !out) return fail(c, RT_ERR_INVALID_ARG, "out is null");
+    if (p->accumulate) {
+        if (!c->sum_valid || c->sum_row_start != start || c->sum_row_step != step ||
+            c->sum_row_count != count || c->sum_samples != p->sample_base)
+            return fail(c, RT_ERR_STATE,
+                        "accumulate: context sum does not hold samples [0, sample_base) of "
+                        "these rows (render with RT_KEEP_SUM first)");
+    }
+    const uint64_t total = (uint64_t)(p->accumulate ? p->sample_base : 0u) + p->spp;
+    if (total == 0 || total > 0xFFFFFFFFull)
+        return fail(c, RT_ERR_INVALID_ARG, "samples in the sum must be in [1, 2^32)");
+
+    const size_t W = (size_t)c->scene.cam.W;
+    const size_t pixels = (size_t)count * W;
+    const size_t px_bytes = (p->flags & RT_OUT_FP16) ? 8u : 16u;
+    hipError_t e;
+    if (keep_sum || p->accumulate) {
+        if (c->sum_cap < pixels) {
+            (void)hipFree(c->d_sum);
+            c->d_sum = nullptr;
+            c->sum_cap = 0;
+            c->sum_valid = false;
+            if ((e = hipMalloc((void**)&c->d_sum, pixels * sizeof(float4))) != hipSuccess)
+                return hip_fail(c, RT_ERR_OUT_OF_MEMORY, "hipMalloc(sum)", e);
+            c->sum_cap = pixels;
+        }
+    }
+    void* kout = nullptr;
+    if (want_out) {
+        if (out_is_device) {
+            kout = out;
+        } else {
+            if (c->out_cap < pixels * px_bytes) {
+                (void)hipFree(c->d_out);
+                c->d_out = nullptr;
+                c->out_cap = 0;
+                if ((e = hipMalloc(&c->d_out, pixels * px_bytes)) != hipSuccess)
+                    return hip_fail(c, RT_ERR_OUT_OF_MEMORY, "hipMalloc(out staging)", e);
+                c->out_cap = pixels * px_bytes;
+            }
+            kout = c->d_out;
+        }
+    }
+
+    rt::KParams K;
+    memset(&K, 0, sizeof(K));
+    K.tri_isect = c->d_tri_isect;
+    K.tri_shade = c->d_tri_shade;
+    K.sph_isect = c->d_sph_isect;
+    K.sph_shade = c->d_sph_shade;
+    K.seeds = c->d_seeds;
+    K.sum = (keep_sum || p->accumulate) ? c->d_sum : nullptr;
+    K.out = kout;
+    K.nT = (uint32_t)c->scene.tri_isect.size();
+    K.nS = (uint32_t)c->scene.sph_isect.size();
+    const rt::CamConst& cam = c->scene.cam;
+    memcpy(K.cam_pos, cam.pos, sizeof(K.cam_pos));
+    memcpy(K.cam_u, cam.u, sizeof(K.cam_u));
+    memcpy(K.cam_v, cam.v, sizeof(K.cam_v));
+    memcpy(K.cam_w, cam.w, sizeof(K.cam_w));
+    K.halfW = cam.halfW;
+    K.halfH = cam.halfH;
+    K.W = cam.W;
+    K.H = cam.H;
+    memcpy(K.light_center, c->scene.light.center, sizeof(K.light_center));
+    memcpy(K.light_color, c->scene.light.color, sizeof(K.light_color));
+    K.spp = p->spp;
+    K.sample_base = p->sample_base;
+    K.row_start = start;
+    K.row_step = step;
+    K.row_count = count;
+    K.accumulate = p->accumulate ? 1u : 0u;
+    K.samples_total = (uint32_t)total;
+    K.flags = (p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u;
+
+    if (keep_sum && !p->accumulate) c->sum_valid = false;  // being overwritten
+    (void)hipEventRecord(c->ev0, stream);
+    e = rt::launch_path_trace(K, p->bounces, stream);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "path_trace launch", e);
+    (void)hipEventRecord(c->ev1, stream);
+    c->timed = true;
+    if (keep_sum || p->accumulate) {  // the kernel (re)wrote the running sums
+        c->sum_valid = true;
+        c->sum_row_start = start;
+        c->sum_row_step = step;
+        c->sum_row_count = count;
+        c->sum_samples = (uint32_t)total;
+    }
+    if (want_out && !out_is_device) {
+        if ((e = hipMemcpyAsync(out, kout, pixels * px_bytes, hipMemcpyDeviceToHost, stream)) !=
+            hipSuccess)
+            return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpyAsync(out)", e);
+    }
+    if (sync) {
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess)
+            return hip_fail(c, RT_ERR_LAUNCH, "path_trace execution", e);
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RTPT_ABI_VERSION; }
+
+const char* rt_status_string(int s) {
+    switch (s) {
+        case RT_OK: return "RT_OK";
+        case RT_ERR_INVALID_ARG: return "RT_ERR_INVALID_ARG";
+        case RT_ERR_NO_DEVICE: return "RT_ERR_NO_DEVICE";
+        case RT_ERR_OUT_OF_MEMORY: return "RT_ERR_OUT_OF_MEMORY";
+        case RT_ERR_LAUNCH: return "RT_ERR_LAUNCH";
+        case RT_ERR_STATE: return "RT_ERR_STATE";
+        case RT_ERR_COMM: return "RT_ERR_COMM";
+        default: return "RT_ERR_UNKNOWN";
+    }
+}
+
+const char* rt_last_error(const rt_ctx* ctx) {
+    return ctx ? ctx->err.c_str() : g_create_err.c_str();
+}
+
+int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
+    if (!out_ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "out_ctx is null");
+    *out_ctx = nullptr;
+    if (!d) return fail(nullptr, RT_ERR_INVALID_ARG, "scene desc is null");
+    if (!d->camera) return fail(nullptr, RT_ERR_INVALID_ARG, "camera is null");
+    if (!d->square_lights || d->n_square_lights < 1)
+        return fail(nullptr, RT_ERR_INVALID_ARG, "square_lights[0] is required (raytrace.metal:22)");
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0)
+        return fail(nullptr, RT_ERR_NO_DEVICE,
+                    std::string("no HIP device: ") + (e != hipSuccess ? hipGetErrorString(e) : "count 0"));
+    if (d->device < 0 || d->device >= count)
+        return fail(nullptr, RT_ERR_NO_DEVICE, "device ordinal out of range");
+
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
+    c->device = d->device;
+    DeviceGuard g(c->device);
+    const char* err = nullptr;
+    if (!rt::compile_scene(*d->camera, d->materials, d->vertices, d->n_triangles,
+                           d->square_lights[0], d->spheres, d->n_spheres, &c->scene, &err)) {
+        delete c;
+        return fail(nullptr, RT_ERR_INVALID_ARG, err);
+    }
+    int status = RT_OK;
+    std::string msg;
+    do {
+        if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+            status = RT_ERR_NO_DEVICE; msg = std::string("hipStreamCreate: ") + hipGetErrorString(e); break;
+        }
+        if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+            status = RT_ERR_NO_DEVICE; msg = std::string("hipEventCreate: ") + hipGetErrorString(e); break;
+        }
+        const rt::CompiledScene& s = c->scene;
+        if ((e = upload(&c->d_tri_isect, s.tri_isect.data(), s.tri_isect.size() * sizeof(rt::TriIsect), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_tri_shade, s.tri_shade.data(), s.tri_shade.size() * sizeof(rt::TriShade), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess) {
+            status = RT_ERR_OUT_OF_MEMORY; msg = std::string("scene upload: ") + hipGetErrorString(e); break;
+        }
+        const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
+        if ((e = hipMalloc((void**)&c->d_seeds, npx * sizeof(uint32_t))) != hipSuccess) {
+            status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(seeds): ") + hipGetErrorString(e); break;
+        }
+    } while (0);
+    if (status != RT_OK) {
+        release(c);
+        delete c;
+        return fail(nullptr, status, msg);
+    }
+    *out_ctx = c;
+    return RT_OK;
+}
+
+int rt_set_seeds(rt_ctx* c, const uint32_t* seeds, int32_t width, int32_t height) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    if (!seeds) return fail(c, RT_ERR_INVALID_ARG, "seeds is null");
+    if (width != c->scene.cam.W || height != c->scene.cam.H)
+        return fail(c, RT_ERR_INVALID_ARG, "seed texture size must equal the camera resolution");
+    DeviceGuard g(c->device);
+    const size_t bytes = (size_t)width * (size_t)height * sizeof(uint32_t);
+    hipError_t e = hipMemcpyAsync(c->d_seeds, seeds, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "seed upload", e);
+    c->seeds_ready = true;
+    return RT_OK;
+}
+
+int rt_fill_seeds(rt_ctx* c, uint64_t key) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    DeviceGuard g(c->device);
+    const uint64_t n = (uint64_t)c->scene.cam.W * (uint64_t)c->scene.cam.H;
+    hipError_t e = rt::launch_fill_seeds(c->d_seeds, key, n, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "fill_seeds", e);
+    c->seeds_ready = true;
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_render_params* p, void* out) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    DeviceGuard g(c->device);
+    const bool dev = p && (p->flags & RT_OUT_DEVICE);
+    return render_impl(c, p, out, dev, c->stream, true);
+}
+
+int rt_render_async(rt_ctx* c, const rt_render_params* p, void* out_device, void* hip_stream) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    DeviceGuard g(c->device);
+    return render_impl(c, p, out_device, true, (hipStream_t)hip_stream, false);
+}
+
+int rt_last_kernel_ms(rt_ctx* c, float* ms) {
+    if (!c || !ms) return fail(c, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->timed) return fail(c, RT_ERR_STATE, "no render yet");
+    DeviceGuard g(c->device);
+    hipError_t e = hipEventSynchronize(c->ev1);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, c->ev0, c->ev1);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "hipEventElapsedTime", e);
+    return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+    if (!c) return RT_OK;
+    release(c);
+    delete c;
+    return RT_OK;
+}
+
+void rt_seed_splitmix(uint64_t key, uint32_t* seeds, size_t n) {
+    if (!seeds) return;
+    for (size_t p = 0; p < n; ++p) seeds[p] = rt::seed_splitmix(key, p);
+}
+
+static void fill_scene_arrays(const rt::Scene& s, CameraGPU* camera, MaterialGPU* materials,
+                              rt_float3* vertices, SquareLightGPU* light) {
+    *camera = rt::convert_camera(s.camera);
+    for (size_t k = 0; k < s.triangles.size(); ++k) {
+        materials[k] = rt::convert_material(s.triangles[k].material);
+        for (int v = 0; v < 3; ++v) vertices[3 * k + v] = rt::to_abi(s.triangles[k].vertices[v]);
+    }
+    *light = rt::convert_square_light(s.light);
+}
+
+int rt_scene_cornell_box(int32_t width, int32_t height, CameraGPU* camera, MaterialGPU* materials,
+                         rt_float3* vertices, SquareLightGPU* light, uint32_t* n_triangles) {
+    if (!camera || !materials || !vertices || !light || !n_triangles || width <= 0 || height <= 0)
+        return RT_ERR_INVALID_ARG;
+    const rt::Scene s = rt::init_cornell_box(width, height);
+    fill_scene_arrays(s, camera, materials, vertices, light);
+    *n_triangles = (uint32_t)s.triangles.size();
+    return RT_OK;
+}
+
+int rt_scene_random_spheres(int32_t width, int32_t height, uint32_t n_spheres, uint64_t seed,
+                            CameraGPU* camera, MaterialGPU* materials, rt_float3* vertices,
+                            SquareLightGPU* light, uint32_t* n_triangles, SphereGPU* spheres) {
+    if (!camera || !materials || !vertices || !light || !n_triangles || width <= 0 ||
+        height <= 0 || (n_spheres && !spheres))
+        return RT_ERR_INVALID_ARG;
+    const rt::Scene s = rt::init_random_spheres(width, height, n_spheres, seed);
+    fill_scene_arrays(s, camera, materials, vertices, light);
+    *n_triangles = (uint32_t)s.triangles.size();
+    for (uint32_t k = 0; k < n_spheres; ++k) spheres[k] = rt::convert_sphere(s.spheres[k]);
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,355 @@
+// rt_kernel.hip — gfx950 path-tracing kernel (the hot path) and its launcher.
+//
+// Rebuilds `kernel pathTrace` (RTrace/raytrace.metal:11-111) for CDNA4:
+//   * the scene's intersection records (triangles 48 B, spheres 16 B) are
+//     staged into LDS once per workgroup and read with wave-uniform addresses
+//     (LDS broadcast); shading records are fetched from global only on a hit;
+//   * one lane per pixel, a wave64 covers an 8x8 pixel tile (the reference's
+//     8x8 threadgroup, renderer.swift:139), a 256-thread workgroup 16x16;
+//   * the bounce loop is unrolled at compile time (template B) so every Halton
+//     dimension, hence every base, is a constant: `i % b` / `i / b` become
+//     magic-number multiplies (exact for u32, so the values are unchanged);
+//   * camera constants are precomputed on the host once (same contract ops);
+//   * the per-pixel result is one coalesced float4 (or half4) store.
+// Arithmetic follows the contract of rt_math.h / DESIGN.md §3 so the result is
+// bit-identical to the CPU oracle.
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include "rt_kernel.hpp"
+
+namespace rt {
+
+namespace {
+
+constexpr uint32_t kPrimes[24] = RT_PRIMES_INIT;
+
+// halton(i, D) — sampling.metal:107-122 with a compile-time dimension.
+template <uint32_t D>
+__device__ __forceinline__ float halton(uint32_t i) {
+    static_assert(D < 24, "Halton dimension outside primes[]");
+    constexpr uint32_t b = kPrimes[D];
+    constexpr float invB = 1.0f / (float)b;
+    float f = 1.0f;
+    float r = 0.0f;
+    while (i > 0) {
+        f = f * invB;
+        r = r + f * (float)(i % b);
+        i = i / b;
+    }
+    return r;
+}
+
+__device__ __forceinline__ f3 ld_f3(const float* p) { return f3{p[0], p[1], p[2]}; }
+
+// Ray/triangle test of DESIGN.md §3.5 (stands in for Metal's intersector).
+__device__ __forceinline__ bool tri_test(const float4& A, const float4& Bq, const float4& C, f3 o,
+                                         f3 d, float tmin, float tmax, float* t_out) {
+    const f3 v0{A.x, A.y, A.z}, e1{A.w, Bq.x, Bq.y}, e2{Bq.z, Bq.w, C.x}, n{C.y, C.z, C.w};
+    const f3 tv = o - v0;
+    const f3 c = cross(tv, d);
+    float den = dot(n, d);
+    float bu = -dot(e2, c);
+    float bv = dot(e1, c);
+    float tn = -dot(n, tv);
+    if (den < 0.0f) {
+        den = -den;
+        bu = -bu;
+        bv = -bv;
+        tn = -tn;
+    }
+    if (den > 0.0f && bu >= 0.0f && bv >= 0.0f && bu + bv <= den) {
+        const float t = tn / den;
+        if (t > tmin && t < tmax) {
+            *t_out = t;
+            return true;
+        }
+    }
+    return false;
+}
+
+// intersectSphere (shaders_old.metal:108-136) with the DESIGN.md §3.6 root rule.
+__device__ __forceinline__ bool sph_test(const float4& S, f3 o, f3 d, float a, float tmin,
+                                         float tmax, float* t_out) {
+    const f3 oc = o - f3{S.x, S.y, S.z};
+    const float b = 2.0f * dot(oc, d);
+    const float cc = dot(oc, oc) - S.w;
+    const float disc = b * b - (4.0f * a) * cc;
+    if (disc > 0.0f) {
+        const float sq = sqrtf(disc);
+        const float a2 = 2.0f * a;
+        const float t1 = (-b - sq) / a2;
+        const float t2 = (-b + sq) / a2;
+        const float t = (t1 > tmin) ? t1 : t2;
+        if (t > tmin && t < tmax) {
+            *t_out = t;
+            return true;
+        }
+    }
+    return false;
+}
+
+// Scene view: intersection records either in LDS (staged) or in global.
+struct SceneView {
+    const float4* tri;  // 3 float4 per triangle
+    const float4* sph;  // 1 float4 per sphere
+    uint32_t nT, nS;
+};
+
+// closest hit, accept_any_intersection(false) (raytrace.metal:48-49)
+template <bool SPH>
+__device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, float tmin,
+                                           float* t_io) {
+    float best = *t_io;
+    int id = -1;
+    for (uint32_t k = 0; k < sv.nT; ++k) {
+        float t;
+        if (tri_test(sv.tri[3 * k], sv.tri[3 * k + 1], sv.tri[3 * k + 2], o, d, tmin, best, &t)) {
+            best = t;
+            id = (int)k;
+        }
+    }
+    if (SPH) {
+        const float a = dot(d, d);
+        for (uint32_t k = 0; k < sv.nS; ++k) {
+            float t;
+            if (sph_test(sv.sph[k], o, d, a, tmin, best, &t)) {
+                best = t;
+                id = (int)(sv.nT + k);
+            }
+        }
+    }
+    *t_io = best;
+    return id;
+}
+
+// any hit, accept_any_intersection(true) (raytrace.metal:79-85).  The boolean
+// result does not depend on the order of the tests.
+template <bool SPH>
+__device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax) {
+    for (uint32_t k = 0; k < sv.nT; ++k) {
+        float t;
+        if (tri_test(sv.tri[3 * k], sv.tri[3 * k + 1], sv.tri[3 * k + 2], o, d, tmin, tmax, &t))
+            return true;
+    }
+    if (SPH) {
+        const float a = dot(d, d);
+        for (uint32_t k = 0; k < sv.nS; ++k) {
+            float t;
+            if (sph_test(sv.sph[k], o, d, a, tmin, tmax, &t)) return true;
+        }
+    }
+    return false;
+}
+
+struct PathState {
+    f3 o, d, acc, thr;
+    uint32_t i;  // Halton index seed + n
+};
+
+// One bounce b of raytrace.metal:47-101.  Returns false when the path ends.
+template <int b, int B, bool SPH>
+__device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, PathState& s) {
+    float t = 1000.0f;                                      // max_distance (sampling.metal:155)
+    const int id = closest_hit<SPH>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
+    if (id < 0) return false;                               // :51-53
+    f3 N, right, fwd, diffuse;
+    if (!SPH || (uint32_t)id < sv.nT) {
+        const float4* sh = P.tri_shade + 4 * id;
+        const float4 s0 = sh[0];
+        const float4 s3 = sh[3];
+        if (s0.w != 0.0f) {                                 // :57-60 light: overwrite, stop
+            s.acc = f3{s3.x, s3.y, s3.z};
+            return false;
+        }
+        const float4 s1 = sh[1], s2 = sh[2];
+        N = f3{s0.x, s0.y, s0.z};
+        right = f3{s1.x, s1.y, s1.z};
+        fwd = f3{s2.x, s2.y, s2.z};
+        diffuse = f3{s1.w, s2.w, s3.w};
+    } else {
+        const uint32_t k = (uint32_t)id - sv.nT;
+        const float4* sh = P.sph_shade + 2 * k;
+        const float4 s0 = sh[0];
+        if (s0.w != 0.0f) {
+            const float4 s1 = sh[1];
+            s.acc = f3{s1.x, s1.y, s1.z};
+            return false;
+        }
+        const float4 S = sv.sph[k];
+        N = normalize((s.o + s.d * t) - f3{S.x, S.y, S.z});
+        shading_frame(N, &right, &fwd);
+        diffuse = f3{s0.x, s0.y, s0.z};
+    }
+    const f3 p = (s.o + s.d * t) + N * 1e-3f;              // :67
+
+    // sampleAreaLight (sampling.metal:198-236), dims 2+5b, 3+5b (:72-74)
+    const float ux = halton<2 + 5 * b>(s.i) * 2.0f - 1.0f;
+    const float uy = halton<3 + 5 * b>(s.i) * 2.0f - 1.0f;
+    const f3 lcen = ld_f3(P.light_center);
+    const f3 q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
+    f3 L = q - p;
+    const float dist = length(L);
+    const float inv = 1.0f / fmaxf(dist, 1e-3f);
+    L = L * inv;
+    f3 lc = ld_f3(P.light_color) * (inv * inv);
+    lc = lc * saturate(dot(-L, f3{0.0f, -1.0f, 0.0f}));
+    lc = lc * saturate(dot(N, L));                         // :75
+    s.thr = s.thr * diffuse;                               // :76
+    if (!any_hit<SPH>(sv, p, L, 0.0f, dist - 1e-3f))       // :79-85
+        s.acc = s.acc + lc * s.thr;                        // :87-89
+    if (b + 1 < B) {                                       // last direction never traced
+        const float cu = halton<4 + 5 * b>(s.i);           // :93-94
+        const float cv = halton<5 + 5 * b>(s.i);
+        float sp, cp;
+        sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
+        const float ct = sqrtf(cv);
+        const float st = sqrtf(1.0f - ct * ct);
+        s.d = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
+        s.o = p;                                           // :99-100
+    }
+    return true;
+}
+
+template <int b, int B, bool SPH>
+struct BounceChain {
+    __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv,
+                                               PathState& s) {
+        if (!bounce<b, B, SPH>(P, sv, s)) return;
+        BounceChain<b + 1, B, SPH>::run(P, sv, s);
+    }
+};
+template <int B, bool SPH>
+struct BounceChain<B, B, SPH> {
+    __device__ __forceinline__ static void run(const KParams&, const SceneView&, PathState&) {}
+};
+
+}  // namespace
+
+template <int B, bool SPH, bool LDS>
+__global__ __launch_bounds__(kBlockThreads) void path_trace_kernel(KParams P) {
+    extern __shared__ float4 lds[];
+    SceneView sv;
+    sv.nT = P.nT;
+    sv.nS = SPH ? P.nS : 0u;
+    if (LDS) {
+        // Stage the intersection records once per workgroup.
+        const uint32_t nt4 = 3u * sv.nT;
+        for (uint32_t k = threadIdx.x; k < nt4; k += kBlockThreads) lds[k] = P.tri_isect[k];
+        if (SPH)
+            for (uint32_t k = threadIdx.x; k < sv.nS; k += kBlockThreads)
+                lds[nt4 + k] = P.sph_isect[k];
+        __syncthreads();
+        sv.tri = lds;
+        sv.sph = lds + nt4;
+    } else {
+        sv.tri = P.tri_isect;
+        sv.sph = P.sph_isect;
+    }
+
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t j = blockIdx.y * kTile + (wave >> 1) * 8u + (lane >> 3);
+    if (x >= (uint32_t)P.W || j >= P.row_count) return;
+    const uint32_t y = P.row_start + j * P.row_step;
+    const size_t o = (size_t)j * (size_t)P.W + x;
+
+    const uint32_t seed = P.seeds[(size_t)y * (size_t)P.W + x];  // raytrace.metal:37
+    f3 lum{0.0f, 0.0f, 0.0f};                                    // :32
+    if (P.accumulate) {
+        const float4 prev = P.sum[o];
+        lum = f3{prev.x, prev.y, prev.z};
+    }
+    const f3 cu = ld_f3(P.cam_u), cv = ld_f3(P.cam_v), cw = ld_f3(P.cam_w);
+    const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
+    for (uint32_t n = 0; n < P.spp; ++n) {                       // :34
+        PathState s;
+        s.i = seed + (P.sample_base + n);
+        const float jx = halton<0>(s.i), jy = halton<1>(s.i);   // :39-40
+        // generateCameraRay (sampling.metal:125-157)
+        const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
+        const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
+        const float sh = sx * P.halfW, th = ty * P.halfH;
+        s.d = normalize((cu * sh + cv * th) - cw);
+        s.o = ld_f3(P.cam_pos);
+        s.acc = f3{0.0f, 0.0f, 0.0f};
+        s.thr = f3{1.0f, 1.0f, 1.0f};
+        BounceChain<0, B, SPH>::run(P, sv, s);                  // :47-102
+        lum = lum + s.acc;                                       // :103
+    }
+    if (P.sum) P.sum[o] = make_float4(lum.x, lum.y, lum.z, (float)P.samples_total);
+    if (P.out) {
+        const float fs = (float)P.samples_total;                 // :106
+        const float r = lum.x / fs, g = lum.y / fs, bl = lum.z / fs;
+        if (P.flags & kOutFp16) {                                // rgba16Float texture
+            ushort4 h;
+            h.x = __half_as_ushort(__float2half_rn(r));
+            h.y = __half_as_ushort(__float2half_rn(g));
+            h.z = __half_as_ushort(__float2half_rn(bl));
+            h.w = __half_as_ushort(__float2half_rn(1.0f));
+            reinterpret_cast<ushort4*>(P.out)[o] = h;
+        } else {
+            reinterpret_cast<float4*>(P.out)[o] = make_float4(r, g, bl, 1.0f);  // :109
+        }
+    }
+}
+
+__global__ void fill_seeds_kernel(uint32_t* seeds, uint64_t key, uint64_t n) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = key + p + 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        z = z ^ (z >> 31);
+        seeds[p] = (uint32_t)(z & 0xFFFFFu);
+    }
+}
+
+namespace {
+
+template <int B, bool SPH, bool LDS>
+hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
+    const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
+    hipLaunchKernelGGL((path_trace_kernel<B, SPH, LDS>), grid, dim3(kBlockThreads),
+                       LDS ? lds_bytes : 0, stream, P);
+    return hipGetLastError();
+}
+
+template <int B>
+hipError_t launch_b(const KParams& P, bool lds, size_t lds_bytes, hipStream_t stream) {
+    const bool sph = P.nS > 0;
+    if (sph) return lds ? launch_t<B, true, true>(P, lds_bytes, stream)
+                        : launch_t<B, true, false>(P, lds_bytes, stream);
+    return lds ? launch_t<B, false, true>(P, lds_bytes, stream)
+               : launch_t<B, false, false>(P, lds_bytes, stream);
+}
+
+}  // namespace
+
+size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_sph) {
+    return (size_t)(3u * n_tri + n_sph) * sizeof(float4);
+}
+
+hipError_t launch_path_trace(const KParams& P, uint32_t bounces, hipStream_t stream) {
+    const size_t lds_bytes = kernel_lds_bytes(P.nT, P.nS);
+    const bool lds = lds_bytes <= kMaxLdsBytes;
+    switch (bounces) {
+        case 0: return launch_b<0>(P, lds, lds_bytes, stream);
+        case 1: return launch_b<1>(P, lds, lds_bytes, stream);
+        case 2: return launch_b<2>(P, lds, lds_bytes, stream);
+        case 3: return launch_b<3>(P, lds, lds_bytes, stream);
+        case 4: return launch_b<4>(P, lds, lds_bytes, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(fill_seeds_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, seeds,
+                       key, n);
+    return hipGetLastError();
+}
+
+}  // namespace rt

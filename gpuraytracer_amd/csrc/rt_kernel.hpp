@@ -1,0 +1,42 @@
+// rt_kernel.hpp — launch interface of the gfx950 path-tracing kernel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_math.h"
+
+namespace rt {
+
+constexpr uint32_t kBlockThreads = 256;  // 4 waves; each wave = 8x8 pixel tile
+constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
+constexpr size_t kMaxLdsBytes = 64 * 1024;
+constexpr uint32_t kOutFp16 = 0x2u;
+
+// Kernel arguments (passed by value -> kernarg segment / SGPRs).
+struct KParams {
+    const float4* tri_isect;  // 3 float4 per triangle (TriIsect)
+    const float4* tri_shade;  // 4 float4 per triangle (TriShade)
+    const float4* sph_isect;  // 1 float4 per sphere   (SphIsect)
+    const float4* sph_shade;  // 2 float4 per sphere   (SphShade)
+    const uint32_t* seeds;    // W*H, full frame
+    float4* sum;              // running sums (tile layout) or null
+    void* out;                // rgba32F / rgba16F tile or null
+    uint32_t nT, nS;
+    float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
+    float halfW, halfH;
+    int32_t W, H;
+    float light_center[3], light_color[3];
+    uint32_t spp, sample_base;
+    uint32_t row_start, row_step, row_count;
+    uint32_t accumulate;      // read P.sum before adding
+    uint32_t samples_total;   // S of `luminance /= samples`
+    uint32_t flags;
+};
+
+size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_sph);
+hipError_t launch_path_trace(const KParams& P, uint32_t bounces, hipStream_t stream);
+hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
+
+}  // namespace rt

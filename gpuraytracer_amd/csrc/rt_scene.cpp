@@ -1,0 +1,321 @@
+// rt_scene.cpp — host scene model, builders and record precompute.
+// Compiled with -ffp-contract=off (see rt_math.h).
+#include "rt_scene.hpp"
+
+#include <string.h>
+
+#include "../../include/rtpt.h"
+
+namespace rt {
+
+namespace {
+
+// Swift's Float.pi is rounded toward zero (0x40490FDA), unlike M_PI_F.
+constexpr float kSwiftPi = 3.14159250f;
+
+f3 from_abi(const rt_float3& v) { return f3{v.x, v.y, v.z}; }
+
+Material make_material(float r, float g, float b, float metallic, float roughness,
+                       f3 emissive = f3{0.0f, 0.0f, 0.0f}) {
+    Material m;
+    m.diffuse[0] = r; m.diffuse[1] = g; m.diffuse[2] = b; m.diffuse[3] = 1.0f;
+    m.metallic = metallic;
+    m.roughness = roughness;
+    m.emissive[0] = emissive.x; m.emissive[1] = emissive.y; m.emissive[2] = emissive.z;
+    return m;
+}
+
+// createRotatedBoxVertices (scene.swift:177-210): simd_float4x4 with columns
+// (c,0,s,0),(0,1,0,0),(-s,0,c,0),(0,0,0,1) applied to (x,y,z,1), then + center.
+void rotated_box(f3 center, float width, float height, float depth, float rot_y, f3 out[8]) {
+    const float hw = width / 2, hh = height / 2, hd = depth / 2;
+    const f3 base[8] = {{-hw, -hh, -hd}, {hw, -hh, -hd}, {hw, hh, -hd}, {-hw, hh, -hd},
+                        {-hw, -hh, hd},  {hw, -hh, hd},  {hw, hh, hd},  {-hw, hh, hd}};
+    // Evaluate cos/sin at run time through the C library (like the oracle), so
+    // no compiler constant-folds them with a differently rounded routine.
+    volatile float angle = rot_y;
+    const float c = cosf(angle), s = sinf(angle);
+    for (int k = 0; k < 8; ++k) {
+        const f3 b = base[k];
+        const float rx = c * b.x + (-s) * b.z;
+        const float rz = s * b.x + c * b.z;
+        out[k] = f3{rx + center.x, b.y + center.y, rz + center.z};
+    }
+}
+
+// createBoxTriangles (scene.swift:212-240)
+void box_triangles(const f3 v[8], const Material& m, std::vector<Triangle>* tris) {
+    static const int faces[12][3] = {{0, 2, 1}, {0, 3, 2}, {4, 5, 6}, {4, 6, 7},
+                                     {0, 4, 7}, {0, 7, 3}, {1, 6, 5}, {1, 2, 6},
+                                     {0, 5, 4}, {0, 1, 5}, {3, 6, 2}, {3, 7, 6}};
+    for (const auto& f : faces) tris->push_back(Triangle{{v[f[0]], v[f[1]], v[f[2]]}, m});
+}
+
+// PCG32 (O'Neill) — generator of the config-4 sphere field.
+struct Pcg32 {
+    uint64_t state = 0, inc = 0;
+    Pcg32(uint64_t initstate, uint64_t initseq) {
+        inc = (initseq << 1u) | 1u;
+        next();
+        state += initstate;
+        next();
+    }
+    uint32_t next() {
+        const uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        const uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((-rot) & 31u));
+    }
+    float uniform(float lo, float hi) {
+        return lo + (hi - lo) * ((float)(next() >> 8) * 5.9604645e-08f);
+    }
+};
+
+}  // namespace
+
+rt_float3 to_abi(f3 v) {
+    rt_float3 r;
+    memset(&r, 0, sizeof(r));
+    r.x = v.x; r.y = v.y; r.z = v.z;
+    return r;
+}
+
+f3 SquareLight::emitted_luminance() const {  // scene.swift:257-270
+    const float flux = luminous_efficacy * watts;
+    const float area = width * depth;
+    const float exitance = flux / area;
+    const float lum = exitance / kSwiftPi;
+    return f3{material.diffuse[0], material.diffuse[1], material.diffuse[2]} * lum;
+}
+
+std::vector<Triangle> create_cornell_box_scene() {
+    std::vector<Triangle> t;
+    const float half = 5.0f / 2.0f;
+    const Material red = make_material(0.9f, 0.0f, 0.0f, 0.05f, 0.3f);
+    const Material green = make_material(0.0f, 0.7f, 0.0f, 0.05f, 0.8f);
+    const Material white = make_material(0.9f, 0.9f, 0.9f, 0.05f, 0.8f);
+    const Material box = make_material(0.9f, 0.9f, 0.9f, 0.05f, 0.3f);
+    const float h = half;
+    // back (:81-90), left/red (:93-102), right/green (:105-114),
+    // floor (:117-126), ceiling (:129-138)
+    t.push_back({{{-h, -h, -h}, {h, h, -h}, {-h, h, -h}}, white});
+    t.push_back({{{-h, -h, -h}, {h, -h, -h}, {h, h, -h}}, white});
+    t.push_back({{{-h, -h, -h}, {-h, h, h}, {-h, -h, h}}, red});
+    t.push_back({{{-h, -h, -h}, {-h, h, -h}, {-h, h, h}}, red});
+    t.push_back({{{h, -h, -h}, {h, h, h}, {h, h, -h}}, green});
+    t.push_back({{{h, -h, -h}, {h, -h, h}, {h, h, h}}, green});
+    t.push_back({{{-h, -h, -h}, {h, -h, h}, {h, -h, -h}}, white});
+    t.push_back({{{-h, -h, -h}, {-h, -h, h}, {h, -h, h}}, white});
+    t.push_back({{{-h, h, -h}, {h, h, h}, {-h, h, h}}, white});
+    t.push_back({{{-h, h, -h}, {h, h, -h}, {h, h, h}}, white});
+    f3 v[8];
+    const float tall_h = 2.8f;  // :141-155
+    rotated_box(f3{-1.0f, -half + tall_h / 2 - 0.05f, -1.5f}, 1.2f, tall_h, 1.2f,
+                kSwiftPi / 2.4f, v);
+    box_triangles(v, box, &t);
+    const float short_h = 1.2f;  // :158-172
+    rotated_box(f3{0.7f, -half + short_h / 2 - 0.05f, 1.2f}, 1.2f, short_h, 1.2f,
+                -kSwiftPi / 2.5f, v);
+    box_triangles(v, box, &t);
+    return t;
+}
+
+Scene init_cornell_box(int32_t width, int32_t height) {
+    Scene s;
+    s.camera.position = f3{0, 0, 9};
+    s.camera.direction = normalize(f3{0, 0, -2.5f} - f3{0, 0, 9});
+    s.camera.up = f3{0, 1, 0};
+    s.camera.resolution[0] = width;
+    s.camera.resolution[1] = height;
+    s.camera.horizontal_fov = kSwiftPi / 4.0f;
+    s.camera.ev100 = 5.0f;
+
+    const float half = 5.0f / 2.0f;
+    const float light_w = 1.0f, light_d = 1.0f;
+    const float light_y = half - 0.01f;
+    const f3 lc{0, light_y, 0};
+    const float hw = light_w / 2, hd = light_d / 2;
+    const f3 v0{lc.x - hw, light_y, lc.z - hd}, v1{lc.x + hw, light_y, lc.z - hd};
+    const f3 v2{lc.x + hw, light_y, lc.z + hd}, v3{lc.x - hw, light_y, lc.z + hd};
+    const Material light_m = make_material(1.0f, 0.95f, 0.9f, 0.0f, 0.0f, f3{1.0f, 1.0f, 1.0f});
+    s.light.center = lc;
+    s.light.vertices[0] = v0; s.light.vertices[1] = v1;
+    s.light.vertices[2] = v2; s.light.vertices[3] = v3;
+    s.light.material = light_m;
+    s.light.luminous_efficacy = 100.0f;
+    s.light.watts = 12.0f;
+    s.light.width = light_w;
+    s.light.depth = light_d;
+
+    s.triangles = create_cornell_box_scene();
+    s.triangles.push_back(Triangle{{v0, v1, v2}, light_m});  // :58-59
+    s.triangles.push_back(Triangle{{v0, v2, v3}, light_m});
+    return s;
+}
+
+Scene init_random_spheres(int32_t width, int32_t height, uint32_t n, uint64_t seed) {
+    Scene s = init_cornell_box(width, height);
+    std::vector<Triangle> kept;
+    for (size_t k = 0; k < s.triangles.size(); ++k)
+        if (k < 10 || k >= 34) kept.push_back(s.triangles[k]);  // walls + light
+    s.triangles = kept;
+    Pcg32 rng(seed, 54u);
+    for (uint32_t i = 0; i < n; ++i) {
+        Sphere sp;
+        const float cx = rng.uniform(-2.3f, 2.3f);
+        const float cy = rng.uniform(-2.3f, 2.2f);
+        const float cz = rng.uniform(-2.3f, 2.3f);
+        const float r = rng.uniform(0.05f, 0.20f);
+        const float ar = rng.uniform(0.1f, 0.9f);
+        const float ag = rng.uniform(0.1f, 0.9f);
+        const float ab = rng.uniform(0.1f, 0.9f);
+        sp.center = f3{cx, cy, cz};
+        sp.radius = r;
+        sp.material = make_material(ar, ag, ab, 0.0f, 1.0f);
+        s.spheres.push_back(sp);
+    }
+    return s;
+}
+
+MaterialGPU convert_material(const Material& m) {
+    MaterialGPU g;
+    memset(&g, 0, sizeof(g));
+    g.diffuse.x = m.diffuse[0]; g.diffuse.y = m.diffuse[1];
+    g.diffuse.z = m.diffuse[2]; g.diffuse.w = m.diffuse[3];
+    g.metallic = m.metallic;
+    g.roughness = m.roughness;
+    g.emissive = to_abi(f3{m.emissive[0], m.emissive[1], m.emissive[2]});
+    return g;
+}
+
+SquareLightGPU convert_square_light(const SquareLight& l) {
+    SquareLightGPU g;
+    memset(&g, 0, sizeof(g));
+    g.center = to_abi(l.center);
+    g.color.x = l.material.diffuse[0]; g.color.y = l.material.diffuse[1];   // color = diffuse
+    g.color.z = l.material.diffuse[2]; g.color.w = l.material.diffuse[3];   // (:36)
+    g.emittedRadiance = to_abi(l.emitted_luminance());
+    g.width = l.width;
+    g.depth = l.depth;
+    return g;
+}
+
+CameraGPU convert_camera(const Camera& c) {
+    CameraGPU g;
+    memset(&g, 0, sizeof(g));
+    g.position = to_abi(c.position);
+    g.direction = to_abi(c.direction);
+    g.up = to_abi(c.up);
+    g.resolution.x = c.resolution[0];
+    g.resolution.y = c.resolution[1];
+    g.horizontalFov = c.horizontal_fov;
+    g.ev100 = c.ev100;
+    return g;
+}
+
+SphereGPU convert_sphere(const Sphere& s) {
+    SphereGPU g;
+    memset(&g, 0, sizeof(g));
+    g.center = to_abi(s.center);
+    g.material = convert_material(s.material);
+    g.radius = s.radius;
+    return g;
+}
+
+uint32_t seed_splitmix(uint64_t key, uint64_t p) {
+    uint64_t z = key + p + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z = z ^ (z >> 31);
+    return (uint32_t)(z & 0xFFFFFu);
+}
+
+static bool finite3(const rt_float3& v) {
+    return isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
+}
+
+bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float3* verts,
+                   uint32_t n_tri, const SquareLightGPU& light, const SphereGPU* spheres,
+                   uint32_t n_sph, CompiledScene* out, const char** err) {
+    if (cam.resolution.x <= 0 || cam.resolution.y <= 0) {
+        *err = "camera resolution must be positive";
+        return false;
+    }
+    if (cam.resolution.x / cam.resolution.y == 0) {
+        // aspectRatio = float(res.x / res.y) (sampling.metal:132) would be 0 and
+        // halfHeight infinite: every ray NaN.  Reject instead of rendering NaNs.
+        *err = "camera resolution.x < resolution.y gives aspectRatio 0 (integer division)";
+        return false;
+    }
+    if (n_tri && (!mats || !verts)) {
+        *err = "materials/vertices must be non-null when n_triangles > 0";
+        return false;
+    }
+    if (n_sph && !spheres) {
+        *err = "spheres must be non-null when n_spheres > 0";
+        return false;
+    }
+    if (!finite3(cam.position) || !finite3(cam.direction) || !finite3(cam.up)) {
+        *err = "camera vectors must be finite";
+        return false;
+    }
+    CamConst& c = out->cam;
+    c.W = cam.resolution.x;
+    c.H = cam.resolution.y;
+    const float aspect = (float)(cam.resolution.x / cam.resolution.y);  // :132
+    c.halfW = tanf(cam.horizontalFov / 2.0f);                            // :133
+    c.halfH = c.halfW / aspect;                                          // :134
+    const f3 w = -normalize(from_abi(cam.direction));                    // :137
+    const f3 u = normalize(cross(from_abi(cam.up), w));                  // :138
+    const f3 v = normalize(cross(w, u));                                 // :139
+    const f3 p = from_abi(cam.position);
+    c.pos[0] = p.x; c.pos[1] = p.y; c.pos[2] = p.z;
+    c.u[0] = u.x; c.u[1] = u.y; c.u[2] = u.z;
+    c.v[0] = v.x; c.v[1] = v.y; c.v[2] = v.z;
+    c.w[0] = w.x; c.w[1] = w.y; c.w[2] = w.z;
+
+    out->light.center[0] = light.center.x;
+    out->light.center[1] = light.center.y;
+    out->light.center[2] = light.center.z;
+    out->light.color[0] = light.color.x;  // squareLights[0].color.xyz (raytrace.metal:22)
+    out->light.color[1] = light.color.y;
+    out->light.color[2] = light.color.z;
+
+    out->tri_isect.resize(n_tri);
+    out->tri_shade.resize(n_tri);
+    for (uint32_t k = 0; k < n_tri; ++k) {
+        const f3 a = from_abi(verts[3 * k]), b = from_abi(verts[3 * k + 1]),
+                 cc = from_abi(verts[3 * k + 2]);
+        const f3 e1 = b - a, e2 = cc - a;        // sampling.metal:23-24
+        const f3 n = cross(e1, e2);
+        const f3 N = normalize(n);               // sampling.metal:25
+        f3 right, fwd;
+        shading_frame(N, &right, &fwd);
+        const f3 em = from_abi(mats[k].emissive);
+        const float light_flag = (length(em) > 0.0f) ? 1.0f : 0.0f;  // raytrace.metal:57
+        const float q[12] = {a.x, a.y, a.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z, n.x, n.y, n.z};
+        memcpy(out->tri_isect[k].q, q, sizeof(q));
+        const float s[16] = {N.x, N.y, N.z, light_flag,
+                             right.x, right.y, right.z, mats[k].diffuse.x,
+                             fwd.x, fwd.y, fwd.z, mats[k].diffuse.y,
+                             em.x, em.y, em.z, mats[k].diffuse.z};
+        memcpy(out->tri_shade[k].s, s, sizeof(s));
+    }
+    out->sph_isect.resize(n_sph);
+    out->sph_shade.resize(n_sph);
+    for (uint32_t k = 0; k < n_sph; ++k) {
+        const SphereGPU& sp = spheres[k];
+        const float r2 = sp.radius * sp.radius;
+        const float q[4] = {sp.center.x, sp.center.y, sp.center.z, r2};
+        memcpy(out->sph_isect[k].q, q, sizeof(q));
+        const f3 em = from_abi(sp.material.emissive);
+        const float light_flag = (length(em) > 0.0f) ? 1.0f : 0.0f;
+        const float s[8] = {sp.material.diffuse.x, sp.material.diffuse.y, sp.material.diffuse.z,
+                            light_flag, em.x, em.y, em.z, 0.0f};
+        memcpy(out->sph_shade[k].s, s, sizeof(s));
+    }
+    return true;
+}
+
+}  // namespace rt

@@ -1,0 +1,122 @@
+// rt_scene.hpp — host-side scene model and the device record layout.
+//
+// Host mirror of the reference's scene/marshalling layer:
+//   RTrace/scene.swift        (Scene, initCornellBox, createCornellBoxScene, ...)
+//   RTrace/computeShader.swift (convertMaterial/convertSquareLight/convertCameras)
+// plus the "compile" step that replaces the Metal BVH build
+// (computeShader.swift:45-97): per-primitive records precomputed once with the
+// contract arithmetic of rt_math.h and staged into LDS by the kernel.
+#pragma once
+
+#include <stdint.h>
+#include <vector>
+
+#include "rt_math.h"
+#include "../../include/rt_types.h"
+
+namespace rt {
+
+// ---- device record layout (all float4-aligned) -------------
+// Triangle intersection record, 3 x float4 = 48 B, staged in LDS:
+//   q0 = (v0.x, v0.y, v0.z, e1.x)  q1 = (e1.y, e1.z, e2.x, e2.y)
+//   q2 = (e2.z, n.x, n.y, n.z)      n = cross(e1, e2) (unnormalized)
+struct TriIsect {
+    float q[12];
+};
+// Triangle shading record, 4 x float4 = 64 B, read from global on a hit:
+//   s0 = (N.xyz, light)  s1 = (right.xyz, diffuse.r)
+//   s2 = (fwd.xyz, diffuse.g)  s3 = (emissive.xyz, diffuse.b)
+struct TriShade {
+    float s[16];
+};
+// Sphere intersection record, 16 B, staged in LDS: (c.xyz, r*r)
+struct SphIsect {
+    float q[4];
+};
+// Sphere shading record, 32 B: (diffuse.rgb, light), (emissive.rgb, 0)
+struct SphShade {
+    float s[8];
+};
+
+// Camera constants of generateCameraRay (sampling.metal:125-157), computed
+// once per scene instead of once per sample (same contract ops).
+struct CamConst {
+    float pos[3], u[3], v[3], w[3];
+    float halfW, halfH;
+    int32_t W, H;
+};
+
+struct LightConst {
+    float center[3], color[3];
+};
+
+struct CompiledScene {
+    CamConst cam;
+    LightConst light;
+    std::vector<TriIsect> tri_isect;
+    std::vector<TriShade> tri_shade;
+    std::vector<SphIsect> sph_isect;
+    std::vector<SphShade> sph_shade;
+};
+
+// Validates and precomputes; returns false with *err set on bad input.
+bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float3* verts,
+                   uint32_t n_tri, const SquareLightGPU& light, const SphereGPU* spheres,
+                   uint32_t n_sph, CompiledScene* out, const char** err);
+
+// ---- scene builders (scene.swift) ------------------------------------------
+struct Material {  // scene.swift:277-282
+    float diffuse[4];
+    float metallic, roughness;
+    float emissive[3];
+};
+
+struct Triangle {  // scene.swift:242-245
+    f3 vertices[3];
+    Material material;
+};
+
+struct SquareLight {  // scene.swift:248-271
+    f3 center;
+    f3 vertices[4];
+    Material material;
+    float luminous_efficacy, watts;  // LightType.bulb
+    float width, depth;
+    f3 emitted_luminance() const;
+};
+
+struct Sphere {  // scene.swift:284-288
+    f3 center;
+    Material material;
+    float radius;
+};
+
+struct Camera {  // scene.swift:290-301
+    f3 position, direction, up;
+    int32_t resolution[2];
+    float horizontal_fov;
+    float ev100;
+};
+
+struct Scene {  // scene.swift:8-12 (+ spheres for config 4)
+    Camera camera;
+    SquareLight light;
+    std::vector<Triangle> triangles;
+    std::vector<Sphere> spheres;
+};
+
+Scene init_cornell_box(int32_t width, int32_t height);                  // scene.swift:14-62
+std::vector<Triangle> create_cornell_box_scene();                       // scene.swift:64-175
+Scene init_random_spheres(int32_t width, int32_t height, uint32_t n, uint64_t seed);
+
+// computeShader.swift conversions
+MaterialGPU convert_material(const Material& m);                        // :13-20
+SquareLightGPU convert_square_light(const SquareLight& l);              // :33-41
+CameraGPU convert_camera(const Camera& c);                              // :242-253
+SphereGPU convert_sphere(const Sphere& s);                              // :232-240
+rt_float3 to_abi(f3 v);
+
+// splitmix64(key + p) mod 2^20 (replaces arc4random, renderer.swift:99-101)
+uint32_t seed_splitmix(uint64_t key, uint64_t p);
+
+}  // namespace rt

@@ -1,0 +1,222 @@
+"""Host-side mirror of the reference's Swift Scene/Renderer API.
+
+``Scene``     <- RTrace/scene.swift (``initCornellBox``, scene.swift:14-62) and
+                 RTrace/computeShader.swift conversions (convertCameras, ...).
+``Renderer``  <- RTrace/renderer.swift: ``__init__`` = ``Renderer.init()``
+                 (:29-115: upload scene, seed texture), ``draw()`` =
+                 ``Renderer.draw()`` (:117-146: dispatch + wait + read back).
+
+Everything executes in librtpt.so (C++ host + gfx950 kernel); this module
+only marshals arrays through ctypes.  Failures raise :class:`RtError` (the
+reference ``fatalError``s).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._native import (RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE,
+                      CameraGPU, MaterialGPU, RenderParamsC, RtError, SceneDesc, SphereGPU,
+                      SquareLightGPU, float3, lib)
+
+DEFAULT_SEED_KEY = 0x5EED00000000
+
+
+def _check(status: int, ctx=None):
+    if status != RT_OK:
+        raise RtError(status, lib.rt_last_error(ctx).decode())
+
+
+def seed_splitmix(width: int, height: int, key: int = DEFAULT_SEED_KEY) -> np.ndarray:
+    """seed[p] = splitmix64(key + p) mod 2^20 — the deterministic stand-in for
+    ``arc4random() % (1024*1024)`` (renderer.swift:99-101)."""
+    n = int(width) * int(height)
+    out = np.empty(n, dtype=np.uint32)
+    lib.rt_seed_splitmix(ctypes.c_uint64(key), out.ctypes.data_as(ctypes.c_void_p), n)
+    return out.reshape(height, width)
+
+
+def tonemap_rgba8(rgba32f: np.ndarray) -> np.ndarray:
+    """image.swift:35-65 epilogue: fp16 round trip, x2 exposure, Reinhard,
+    gamma 1/2.2, truncating UInt8 (alpha 255)."""
+    a = np.ascontiguousarray(rgba32f, dtype=np.float32)
+    n = a.size // 4
+    out = np.empty(a.shape[:-1] + (4,), dtype=np.uint8)
+    lib.rt_tonemap_rgba8(a.ctypes.data_as(ctypes.c_void_p), n,
+                         out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+class Scene:
+    """The shaderTypes.h arrays of one scene (what Renderer.init uploads)."""
+
+    def __init__(self, camera: CameraGPU, materials, vertices, light: SquareLightGPU,
+                 spheres=None):
+        self.camera = camera
+        self.materials = materials            # (MaterialGPU * n_tri)
+        self.vertices = vertices              # (float3 * 3n_tri), 16-B stride
+        self.light = light
+        self.spheres = spheres                # (SphereGPU * n_sph) or None
+
+    @property
+    def n_triangles(self) -> int:
+        return len(self.materials)
+
+    @property
+    def n_spheres(self) -> int:
+        return 0 if self.spheres is None else len(self.spheres)
+
+    @property
+    def width(self) -> int:
+        return int(self.camera.resolution.x)
+
+    @property
+    def height(self) -> int:
+        return int(self.camera.resolution.y)
+
+    @classmethod
+    def cornell_box(cls, width: int = 800, height: int = 600) -> "Scene":
+        """initCornellBox() (scene.swift:14-62), resolution overridden."""
+        cam, light = CameraGPU(), SquareLightGPU()
+        mats = (MaterialGPU * 36)()
+        verts = (float3 * 108)()
+        n = ctypes.c_uint32()
+        _check(lib.rt_scene_cornell_box(width, height, ctypes.byref(cam), mats, verts,
+                                        ctypes.byref(light), ctypes.byref(n)))
+        assert n.value == 36
+        return cls(cam, mats, verts, light)
+
+    @classmethod
+    def random_spheres(cls, width: int = 1920, height: int = 1080, n_spheres: int = 1000,
+                       seed: int = 42) -> "Scene":
+        """Config-4 scene: Cornell walls + light + PCG32(seed) spheres."""
+        cam, light = CameraGPU(), SquareLightGPU()
+        mats = (MaterialGPU * 12)()
+        verts = (float3 * 36)()
+        sph = (SphereGPU * max(n_spheres, 1))()
+        n = ctypes.c_uint32()
+        _check(lib.rt_scene_random_spheres(width, height, n_spheres, ctypes.c_uint64(seed),
+                                           ctypes.byref(cam), mats, verts, ctypes.byref(light),
+                                           ctypes.byref(n), sph))
+        return cls(cam, mats, verts, light, sph if n_spheres else None)
+
+    def desc(self, device: int = 0) -> SceneDesc:
+        d = SceneDesc()
+        d.camera = ctypes.pointer(self.camera)
+        d.materials = ctypes.cast(self.materials, ctypes.POINTER(MaterialGPU))
+        d.square_lights = ctypes.pointer(self.light)
+        d.n_square_lights = 1
+        d.vertices = ctypes.cast(self.vertices, ctypes.POINTER(float3))
+        d.n_triangles = self.n_triangles
+        if self.spheres is not None:
+            d.spheres = ctypes.cast(self.spheres, ctypes.POINTER(SphereGPU))
+            d.n_spheres = self.n_spheres
+        d.device = device
+        return d
+
+
+@dataclass
+class RenderParams:
+    """rt_render_params (include/rtpt.h)."""
+
+    spp: int = 400          # raytrace.metal:24
+    bounces: int = 3        # raytrace.metal:25
+    sample_base: int = 0
+    row_start: int = 0
+    row_step: int = 1
+    row_count: int = 0      # 0 = every row from row_start with row_step
+    accumulate: bool = False
+    keep_sum: bool = False
+    fp16: bool = False
+
+    def c(self, flags: int = 0) -> RenderParamsC:
+        p = RenderParamsC()
+        p.spp, p.bounces, p.sample_base = self.spp, self.bounces, self.sample_base
+        p.row_start, p.row_step, p.row_count = self.row_start, self.row_step, self.row_count
+        p.accumulate = 1 if self.accumulate else 0
+        p.flags = flags | (RT_KEEP_SUM if self.keep_sum else 0) | (RT_OUT_FP16 if self.fp16 else 0)
+        return p
+
+    def rows(self, height: int) -> int:
+        if self.row_count:
+            return self.row_count
+        step = self.row_step or 1
+        return (height - 1 - self.row_start) // step + 1
+
+
+class Renderer:
+    """renderer.swift's Renderer on the MI355X C-ABI."""
+
+    def __init__(self, scene: Scene, device: int = 0, seeds=None,
+                 seed_key: int = DEFAULT_SEED_KEY):
+        self.scene = scene
+        self.device = device
+        ctx = ctypes.c_void_p()
+        _check(lib.rt_create(ctypes.byref(scene.desc(device)), ctypes.byref(ctx)))
+        self._ctx = ctx
+        if seeds is not None:
+            s = np.ascontiguousarray(seeds, dtype=np.uint32)
+            if s.size != scene.width * scene.height:
+                raise ValueError("seed texture must have width*height entries")
+            _check(lib.rt_set_seeds(ctx, s.ctypes.data_as(ctypes.c_void_p), scene.width,
+                                    scene.height), ctx)
+        else:
+            _check(lib.rt_fill_seeds(ctx, ctypes.c_uint64(seed_key)), ctx)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib.rt_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_seeds(self, seeds):
+        s = np.ascontiguousarray(seeds, dtype=np.uint32)
+        _check(lib.rt_set_seeds(self._ctx, s.ctypes.data_as(ctypes.c_void_p), self.scene.width,
+                                self.scene.height), self._ctx)
+
+    def render(self, params: RenderParams | None = None, out=None, stream=None):
+        """Render into host memory (returns (rows, W, 4) float32, or uint16
+        bits for fp16), or into a device tensor ``out`` (anything with
+        ``data_ptr()``) enqueued on ``stream`` (a raw hipStream_t int / torch
+        stream; default torch's current stream) without a host sync."""
+        p = params or RenderParams()
+        if out is None:
+            rows = p.rows(self.scene.height)
+            dt = np.uint16 if p.fp16 else np.float32
+            img = np.empty((rows, self.scene.width, 4), dtype=dt)
+            _check(lib.rt_render(self._ctx, ctypes.byref(p.c()),
+                                 img.ctypes.data_as(ctypes.c_void_p)), self._ctx)
+            return img
+        if stream is None:
+            import torch  # plumbing only: the stream the caller's events see
+            stream = torch.cuda.current_stream().cuda_stream
+        elif hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        ptr = out if isinstance(out, int) else out.data_ptr()
+        _check(lib.rt_render_async(self._ctx, ctypes.byref(p.c(RT_OUT_DEVICE)),
+                                   ctypes.c_void_p(ptr), ctypes.c_void_p(stream)), self._ctx)
+        return out
+
+    def accumulate(self, params: RenderParams):
+        """Add samples to the context's running sums only (no image output)."""
+        _check(lib.rt_render(self._ctx, ctypes.byref(params.c(RT_OUT_NONE | RT_KEEP_SUM)), None),
+               self._ctx)
+
+    def draw(self, spp: int = 400, bounces: int = 3) -> np.ndarray:
+        """Renderer.draw(): the whole frame, synchronously; (H, W, 4) float32."""
+        return self.render(RenderParams(spp=spp, bounces=bounces))
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float()
+        _check(lib.rt_last_kernel_ms(self._ctx, ctypes.byref(ms)), self._ctx)
+        return float(ms.value)

@@ -1,0 +1,259 @@
+"""CPU: the oracle against known answers, the independent numpy restatement,
+the committed golden fixtures, and the reference's own PNG geometry."""
+import ctypes
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from gpuraytracer_amd import Scene
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+L = oracle_lib.lib
+F3 = ctypes.c_float * 3
+
+
+def f3(*v):
+    return F3(*v)
+
+
+# ---- halton (sampling.metal:107-122) ---------------------------------------
+@pytest.mark.parametrize("i,d,expect", [
+    (0, 0, 0.0), (1, 0, 0.5), (2, 0, 0.25), (3, 0, 0.75), (4, 0, 0.125),
+    (1, 1, np.float32(1 / 3)), (2, 1, np.float32(2 / 3)),
+    (3, 1, np.float32(1 / 3) * np.float32(1 / 3)),  # f = invB*invB rounded in fp32
+    (1, 2, np.float32(0.2)),
+])
+def test_halton_known_answers(i, d, expect):
+    assert np.float32(oracle_lib.halton(i, d)) == np.float32(expect)
+
+
+def test_halton_base2_is_bit_reversal():
+    # for base 2 every partial sum is exact: radical inverse == bitreverse(i) / 2^32
+    for i in [1, 5, 123457, 2**20 - 1, 2**23 + 11]:
+        rev = int(f"{i:032b}"[::-1], 2)
+        assert np.float32(oracle_lib.halton(i, 0)) == np.float32(rev / 2.0**32)
+
+
+def test_halton_loop_order_matches_numpy():
+    import pt_oracle_np as P
+    i = np.array([0, 1, 7, 999, 2**20 - 1, 2**20 + 399, 2**31 + 5, 2**32 - 1], np.uint32)
+    for d in range(24):
+        c = np.array([oracle_lib.halton(int(v), d) for v in i], np.float32)
+        assert np.array_equal(c.view(np.uint32), P.halton(i, d).view(np.uint32)), d
+
+
+# ---- portable sincos ---------------------------------------------------------
+def test_sincos_accuracy_and_quadrants():
+    s, c = ctypes.c_float(), ctypes.c_float()
+    xs = np.linspace(0, 2 * np.pi, 20001, dtype=np.float32)
+    err = 0.0
+    for x in xs[::7]:
+        L.pto_sincos(ctypes.c_float(x), ctypes.byref(s), ctypes.byref(c))
+        err = max(err, abs(s.value - math.sin(float(x))), abs(c.value - math.cos(float(x))))
+    assert err < 4e-7
+    L.pto_sincos(ctypes.c_float(0.0), ctypes.byref(s), ctypes.byref(c))
+    assert (s.value, c.value) == (0.0, 1.0)
+
+
+def test_sincos_matches_numpy_restatement():
+    import pt_oracle_np as P
+    xs = (np.random.default_rng(1).random(4000) * np.float32(6.28318548)).astype(np.float32)
+    sn, cn = P.sincos(xs)
+    s, c = ctypes.c_float(), ctypes.c_float()
+    for k, x in enumerate(xs):
+        L.pto_sincos(ctypes.c_float(x), ctypes.byref(s), ctypes.byref(c))
+        assert np.float32(s.value) == sn[k] and np.float32(c.value) == cn[k]
+
+
+# ---- ray / primitive tests ---------------------------------------------------
+def tri(o, d, v0, v1, v2, tmin=0.001, tmax=1000.0):
+    t = ctypes.c_float()
+    L.pto_ray_triangle.restype = ctypes.c_int
+    L.pto_ray_triangle.argtypes = [F3, F3, F3, F3, F3, ctypes.c_float, ctypes.c_float,
+                                   ctypes.POINTER(ctypes.c_float)]
+    hit = L.pto_ray_triangle(f3(*o), f3(*d), f3(*v0), f3(*v1), f3(*v2), tmin, tmax, ctypes.byref(t))
+    return hit, t.value
+
+
+def test_ray_triangle_hit_miss_and_both_faces():
+    v0, v1, v2 = (0, 0, 0), (1, 0, 0), (0, 1, 0)
+    hit, t = tri((0.25, 0.25, 5), (0, 0, -1), v0, v1, v2)
+    assert hit and t == 5.0
+    hit, t = tri((0.25, 0.25, -5), (0, 0, 1), v0, v1, v2)   # back face: no culling
+    assert hit and t == 5.0
+    assert not tri((0.8, 0.8, 5), (0, 0, -1), v0, v1, v2)[0]  # outside u+v<=1
+    assert not tri((0.25, 0.25, 5), (1, 0, 0), v0, v1, v2)[0]  # parallel: det == 0
+    assert not tri((0.25, 0.25, 5), (0, 0, 1), v0, v1, v2)[0]  # behind origin
+    assert not tri((0.25, 0.25, 5), (0, 0, -1), v0, v1, v2, tmax=5.0)[0]  # t < tmax strict
+    hit, _ = tri((0.0, 0.0, 5), (0, 0, -1), v0, v1, v2)      # vertex: edges inclusive
+    assert hit
+
+
+def sph(o, d, c, r, tmin=0.001, tmax=1000.0):
+    t = ctypes.c_float()
+    L.pto_ray_sphere.restype = ctypes.c_int
+    L.pto_ray_sphere.argtypes = [F3, F3, F3, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                 ctypes.POINTER(ctypes.c_float)]
+    return L.pto_ray_sphere(f3(*o), f3(*d), f3(*c), r, tmin, tmax, ctypes.byref(t)), t.value
+
+
+def test_ray_sphere_front_inside_behind_tangent():
+    hit, t = sph((0, 0, 5), (0, 0, -1), (0, 0, 0), 1.0)
+    assert hit and t == 4.0
+    hit, t = sph((0, 0, 0), (0, 0, -1), (0, 0, 0), 1.0)       # inside: far root (corrected rule)
+    assert hit and t == 1.0
+    assert not sph((0, 0, 5), (0, 0, 1), (0, 0, 0), 1.0)[0]    # sphere behind the ray
+    assert not sph((1, 0, 5), (0, 0, -1), (0, 0, 0), 1.0)[0]   # tangent: disc == 0 is a miss
+    hit, t = sph((0, 0, 5), (0, 0, -2), (0, 0, 0), 1.0)       # un-normalised direction
+    assert hit and t == 2.0
+
+
+# ---- camera / light / cosine sample ----------------------------------------------
+def test_camera_center_and_corner_rays():
+    cam, *_ = oracle_lib.cornell_box(800, 600)
+    d = F3()
+    L.pto_camera_ray.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                 ctypes.c_float, F3]
+    L.pto_camera_ray(ctypes.byref(cam), 400, 300, 0.0, 0.0, d)
+    assert list(d) == [0.0, 0.0, -1.0]                          # basis u=(1,0,0) v=(0,1,0) w=(0,0,1)
+    L.pto_camera_ray(ctypes.byref(cam), 0, 0, 0.0, 0.0, d)
+    hw = np.float32(math.tan(np.float32(np.float32(3.1415925) / 4) / 2))
+    # aspect = float(800/600) = 1 (integer division, sampling.metal:132) -> halfH == halfW
+    v = np.array([-hw, hw, -1.0]) / np.linalg.norm([-hw, hw, -1.0])
+    assert np.allclose(list(d), v, atol=1e-6)
+
+
+def test_area_light_directly_below():
+    _, _, _, light, _ = oracle_lib.cornell_box(8, 8)
+    ldir, col, dist = F3(), F3(), ctypes.c_float()
+    L.pto_sample_area_light.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, F3, F3,
+                                        ctypes.POINTER(ctypes.c_float), F3]
+    L.pto_sample_area_light(ctypes.byref(light), 0.5, 0.5, f3(0, 0.49, 0), ldir, ctypes.byref(dist), col)
+    assert list(ldir) == [0.0, 1.0, 0.0] and np.float32(dist.value) == np.float32(2.0)
+    # color = (1, .95, .9) / dist^2 * cos(0) (sampling.metal:226-233)
+    assert np.allclose(list(col), np.array([1.0, 0.95, 0.9]) / 4.0, rtol=1e-6)
+
+
+def test_cosine_sample_pole_is_normal():
+    d = F3()
+    L.pto_cosine_direction.argtypes = [ctypes.c_float, ctypes.c_float, F3, F3]
+    for n in [(0, 1, 0), (1, 0, 0), (0, 0, -1)]:
+        L.pto_cosine_direction(0.0, 1.0, f3(*n), d)
+        assert np.allclose(list(d), n, atol=1e-7)
+
+
+# ---- scene builders ---------------------------------------------------------------
+def test_cornell_scene_matches_appendix_b():
+    cam, mats, verts, light, n = oracle_lib.cornell_box(800, 600)
+    assert n == 36
+    v = np.frombuffer(bytes(verts), np.float32).reshape(108, 4)[:, :3]
+    m = np.frombuffer(bytes(mats), np.float32).reshape(36, 12)
+    assert np.array_equal(v[0:3], [[-2.5, -2.5, -2.5], [2.5, 2.5, -2.5], [-2.5, 2.5, -2.5]])
+    ly = np.float32(2.5) - np.float32(0.01)  # lightY = half - 0.01 in Float (scene.swift:25)
+    assert np.array_equal(v[102:105], np.array([[-0.5, ly, -0.5], [0.5, ly, -0.5], [0.5, ly, 0.5]],
+                                               np.float32))
+    assert np.allclose(m[2, :3], [0.9, 0, 0]) and np.allclose(m[4, :3], [0, 0.7, 0])   # red/green
+    assert np.array_equal(m[34, 8:11], [1, 1, 1]) and np.all(m[:34, 8:11] == 0)          # emissive
+    assert light.center.y == ly and light.color.y == np.float32(0.95)
+    assert cam.resolution.x == 800 and cam.horizontalFov == np.float32(3.1415925) / 4
+    # boxes inside the room in x/z; their bottoms sit 0.05 below the floor
+    # (centre y = -half + h/2 - 0.05, scene.swift:144,160)
+    assert np.abs(v[30:102][:, [0, 2]]).max() <= 2.5
+    assert np.float32(v[30:66, 1].min()) == np.float32(-2.55)
+
+
+def test_product_scene_builder_equals_oracle():
+    for w, h in [(800, 600), (1920, 1080), (17, 9)]:
+        s = Scene.cornell_box(w, h)
+        cam, mats, verts, light, n = oracle_lib.cornell_box(w, h)
+        assert bytes(s.camera) == bytes(cam)
+        assert bytes(s.materials) == bytes(mats)
+        assert bytes(s.vertices) == bytes(verts)
+        assert bytes(s.light) == bytes(light)
+    s = Scene.random_spheres(64, 32, 1000, seed=42)
+    cam, mats, verts, light, n, sph_ = oracle_lib.random_spheres(64, 32, 1000, seed=42)
+    assert n == 12 and bytes(s.vertices) == bytes(verts) and bytes(s.spheres) == bytes(sph_)
+    r = np.frombuffer(bytes(sph_), np.float32).reshape(1000, 20)
+    assert r[:, 16].min() >= 0.05 and r[:, 16].max() <= 0.2
+    assert r[:, 0].min() >= -2.3 and r[:, 1].max() <= 2.2
+
+
+def test_seed_function_matches_product_and_range():
+    from gpuraytracer_amd import seed_splitmix
+    a = oracle_lib.seeds(37, 11)
+    b = seed_splitmix(37, 11)
+    assert np.array_equal(a, b) and a.max() < 2**20 and len(np.unique(a)) > 390
+
+
+# ---- renders ----------------------------------------------------------------------
+def test_oracle_equals_numpy_restatement_8x8():
+    import pt_oracle_np as P
+    s = Scene.cornell_box(8, 8)
+    sd = oracle_lib.seeds(8, 8)
+    for bounces in (1, 2, 3, 4):
+        out = oracle_lib.render(s, sd, 2, bounces)
+        sc = P.Scene(s.camera, s.materials, s.light, s.vertices)
+        ref = P.render(sc, sd, 2, bounces)
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), bounces
+
+
+@pytest.mark.parametrize("name", ["cornell_16x16_s4_b3", "cornell_128x128_s1_b3",
+                                  "cornell_24x13_s3_b4_u32seeds", "spheres60_16x16_s2_b3"])
+def test_oracle_reproduces_golden(name):
+    from gpuraytracer_amd import CameraGPU, MaterialGPU, SphereGPU, SquareLightGPU, float3
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    cam = CameraGPU.from_buffer_copy(g["camera"].tobytes())
+    light = SquareLightGPU.from_buffer_copy(g["light"].tobytes())
+    mats = (MaterialGPU * (len(g["materials"]) // 48)).from_buffer_copy(g["materials"].tobytes())
+    verts = (float3 * (len(g["vertices"]) // 16)).from_buffer_copy(g["vertices"].tobytes())
+    sph_ = None
+    if "spheres" in g:
+        sph_ = (SphereGPU * (len(g["spheres"]) // 80)).from_buffer_copy(g["spheres"].tobytes())
+    s = Scene(cam, mats, verts, light, sph_)
+    spp, bounces, base = (int(v) for v in g["params"])
+    out = oracle_lib.render(s, g["seeds"], spp, bounces, sample_base=base)
+    assert np.array_equal(out.view(np.uint32), g["out"].view(np.uint32))
+
+
+def test_batched_equals_single_shot_and_rows():
+    s = Scene.cornell_box(20, 12)
+    sd = oracle_lib.seeds(20, 12)
+    full = oracle_lib.render(s, sd, 6, 3)
+    _, s1 = oracle_lib.render(s, sd, 2, 3, want_sum=True)
+    _, s2 = oracle_lib.render(s, sd, 3, 3, sample_base=2, sum_in=s1, want_sum=True)
+    out3 = oracle_lib.render(s, sd, 1, 3, sample_base=5, sum_in=s2)
+    assert np.array_equal(out3.view(np.uint32), full.view(np.uint32))
+    tile = oracle_lib.render(s, sd, 6, 3, row_start=1, row_step=3)
+    assert np.array_equal(tile.view(np.uint32), full[1::3].view(np.uint32))
+
+
+def test_light_footprint_matches_reference_png():
+    """example.png (reference, README.md:1) is an earlier revision, but its
+    light footprint pins the camera + light geometry of the live scene."""
+    fp = json.load(open(os.path.join(GOLDEN, "footprint.json")))
+    W, H = fp["width"], fp["height"]
+    s = Scene.cornell_box(W, H)
+    sd = oracle_lib.seeds(W, H)
+    y0, y1 = fp["rows"]
+    x0, x1 = fp["cols"]
+    band = oracle_lib.render(s, sd, 1, 1, row_start=y0 - 6, row_count=(y1 - y0) + 13)
+    lit = np.all(band[..., :3] == 1.0, axis=-1)  # emissive (1,1,1) overwrite on a light hit
+    ys, xs = np.nonzero(lit)
+    ys = ys + y0 - 6
+    assert abs(int(ys.min()) - y0) <= 2 and abs(int(ys.max()) - y1) <= 2
+    assert abs(int(xs.min()) - x0) <= 3 and abs(int(xs.max()) - x1) <= 3
+    corner = oracle_lib.render(s, sd, 1, 3, row_count=1)[0, 0]
+    assert np.all(corner[:3] == 0.0) and fp["corner_rgb"] == [0, 0, 0]
+
+
+def test_tonemap_matches_image_swift():
+    from gpuraytracer_amd import tonemap_rgba8
+    x = np.random.default_rng(3).random((64, 4), dtype=np.float32) * 3
+    x[0, :3] = [0.0, 1.0, 70000.0]  # fp16 overflow -> inf -> 1.0 -> 255
+    a, b = tonemap_rgba8(x), oracle_lib.tonemap(x)
+    assert np.array_equal(a, b)
+    assert list(a[0]) == [0, 212, 255, 255]  # 1.0 -> (2/3)^(1/2.2)*255 = 212
