@@ -11,7 +11,7 @@ SRC := $(PKG)/csrc
 BLD := build
 COMMON := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude
 HOSTCXX ?= /opt/rocm/llvm/bin/clang++
-HIPFLAGS := $(COMMON) --offload-arch=$(ARCH)
+HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-slp-vectorize
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include
 
 OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -36,6 +37,7 @@ struct rt_ctx {
     size_t out_cap = 0;     // bytes
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=lds|smem (tuning knob)
     std::string err;
 };
 
@@ -195,7 +197,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
 
     if (keep_sum && !p->accumulate) c->sum_valid = false;  // being overwritten
     (void)hipEventRecord(c->ev0, stream);
-    e = rt::launch_path_trace(K, p->bounces, stream);
+    e = rt::launch_path_trace(K, p->bounces, c->scene_mem, stream);
     if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "path_trace launch", e);
     (void)hipEventRecord(c->ev1, stream);
     c->timed = true;
@@ -259,6 +261,10 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
     c->device = d->device;
+    if (const char* m = getenv("RTPT_SCENE_MEM")) {
+        if (!strcmp(m, "lds")) c->scene_mem = rt::SceneMem::kLds;
+        if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
+    }
     DeviceGuard g(c->device);
     const char* err = nullptr;
     if (!rt::compile_scene(*d->camera, d->materials, d->vertices, d->n_triangles,

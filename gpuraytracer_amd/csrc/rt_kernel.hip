@@ -43,23 +43,23 @@ __device__ __forceinline__ float halton(uint32_t i) {
 __device__ __forceinline__ f3 ld_f3(const float* p) { return f3{p[0], p[1], p[2]}; }
 
 // Ray/triangle test of DESIGN.md §3.5 (stands in for Metal's intersector).
+// The oracle negates (bu, bv, tn, den) when den < 0; here the same exact
+// negation is an XOR with den's sign bit, |den| folds into the compare, and tn
+// (with the IEEE division) is only formed for lanes inside the triangle.
 __device__ __forceinline__ bool tri_test(const float4& A, const float4& Bq, const float4& C, f3 o,
                                          f3 d, float tmin, float tmax, float* t_out) {
     const f3 v0{A.x, A.y, A.z}, e1{A.w, Bq.x, Bq.y}, e2{Bq.z, Bq.w, C.x}, n{C.y, C.z, C.w};
     const f3 tv = o - v0;
     const f3 c = cross(tv, d);
-    float den = dot(n, d);
-    float bu = -dot(e2, c);
-    float bv = dot(e1, c);
-    float tn = -dot(n, tv);
-    if (den < 0.0f) {
-        den = -den;
-        bu = -bu;
-        bv = -bv;
-        tn = -tn;
-    }
-    if (den > 0.0f && bu >= 0.0f && bv >= 0.0f && bu + bv <= den) {
-        const float t = tn / den;
+    const float den = dot(n, d);
+    const uint32_t sgn = __float_as_uint(den) & 0x80000000u;
+    const uint32_t nsgn = sgn ^ 0x80000000u;
+    const float bu = __uint_as_float(__float_as_uint(dot(e2, c)) ^ nsgn);  // -dot(e2,c), sign-normalised
+    const float bv = __uint_as_float(__float_as_uint(dot(e1, c)) ^ sgn);
+    const float aden = fabsf(den);
+    if (aden > 0.0f && bu >= 0.0f && bv >= 0.0f && bu + bv <= aden) {
+        const float tn = __uint_as_float(__float_as_uint(dot(n, tv)) ^ nsgn);  // -dot(n,tv)
+        const float t = tn / aden;
         if (t > tmin && t < tmax) {
             *t_out = t;
             return true;
@@ -330,9 +330,10 @@ size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_sph) {
     return (size_t)(3u * n_tri + n_sph) * sizeof(float4);
 }
 
-hipError_t launch_path_trace(const KParams& P, uint32_t bounces, hipStream_t stream) {
+hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
+                             hipStream_t stream) {
     const size_t lds_bytes = kernel_lds_bytes(P.nT, P.nS);
-    const bool lds = lds_bytes <= kMaxLdsBytes;
+    const bool lds = lds_bytes <= kMaxLdsBytes && mem != SceneMem::kSmem;
     switch (bounces) {
         case 0: return launch_b<0>(P, lds, lds_bytes, stream);
         case 1: return launch_b<1>(P, lds, lds_bytes, stream);

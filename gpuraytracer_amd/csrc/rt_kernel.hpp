@@ -36,7 +36,9 @@ struct KParams {
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_sph);
-hipError_t launch_path_trace(const KParams& P, uint32_t bounces, hipStream_t stream);
+// Where the workgroup reads the intersection records from.
+enum class SceneMem { kAuto = 0, kLds = 1, kSmem = 2 };
+hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 
 }  // namespace rt

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh output directory into one JSON object.
+
+    summarize_profile.py <prof_dir> [bench.py args...]
+
+Per-launch averages for the path_trace kernel: duration from the kernel
+trace, every PMC counter from the --pmc passes, and the derived HBM traffic:
+bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM: on
+gfx950 FETCH_SIZE reports half of a wide streaming read; counters in KiB).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNEL = "path_trace"
+
+
+def bench_workload(argv):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--spheres", type=int, default=1000)
+    a, _ = ap.parse_known_args(argv)
+    if a.scene == "cornell":
+        return f"cornell_{a.width}x{a.height}_{a.spp}spp_b{a.bounces}"
+    return f"spheres{a.spheres}_{a.width}x{a.height}_{a.spp}spp_b{a.bounces}"
+
+
+def rows(pattern):
+    for path in glob.glob(pattern, recursive=True):
+        with open(path, newline="") as f:
+            yield from csv.DictReader(f)
+
+
+def main():
+    d = sys.argv[1]
+    out = {"workload": bench_workload(sys.argv[2:]), "n_gpus": 1, "kernel": None}
+    durs = []
+    for r in rows(os.path.join(d, "trace", "**", "*kernel_trace.csv")):
+        if KERNEL in r.get("Kernel_Name", ""):
+            out["kernel"] = r["Kernel_Name"]
+            durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            for k in ("VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "LDS_Block_Size",
+                      "Scratch_Size", "Workgroup_Size", "Grid_Size"):
+                if k in r:
+                    out.setdefault("resources", {})[k] = r[k]
+    if durs:
+        out["launches_traced"] = len(durs)
+        out["avg_ns"] = sum(durs) / len(durs)
+        out["min_ns"] = min(durs)
+        out["max_ns"] = max(durs)
+    stats = []
+    for r in rows(os.path.join(d, "trace", "**", "*kernel_stats.csv")):
+        stats.append({k: r[k] for k in r})
+    out["kernel_stats"] = stats
+    counters = defaultdict(list)
+    for r in rows(os.path.join(d, "*", "**", "*counter_collection.csv")):
+        if KERNEL in r.get("Kernel_Name", ""):
+            counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out["counters_per_launch"] = {k: sum(v) / len(v) for k, v in sorted(counters.items())}
+    c = out["counters_per_launch"]
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["hbm_bytes_per_launch_raw"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        out["hbm_bytes_per_launch"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+    if "SQ_INSTS_VALU" in c:
+        out["sq_insts_valu_per_launch"] = c["SQ_INSTS_VALU"]
+    if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
+        out["valu_lane_utilization"] = c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"])
+    if "GRBM_GUI_ACTIVE" in c and durs:
+        # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall (MI355X_MICROARCH.md DVFS note)
+        out["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / out["avg_ns"]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
