@@ -83,6 +83,11 @@ class RenderParamsC(ctypes.Structure):  # rt_render_params
                  "accumulate", "flags")]
 
 
+class SceneInfo(ctypes.Structure):  # rt_scene_info
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                ("n_triangles", "n_triangle_pairs", "n_spheres", "lds_bytes")]
+
+
 RT_OK = 0
 RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE, RT_KEEP_SUM = 0x1, 0x2, 0x4, 0x8
 RT_MAX_BOUNCES = 4
@@ -117,6 +122,7 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_uint32),
                                                ctypes.POINTER(SphereGPU)]),
     "rt_tonemap_rgba8": (None, [_P, ctypes.c_size_t, _P]),
+    "rt_scene_describe": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(SceneInfo)]),
 }
 
 

@@ -25,6 +25,7 @@ struct rt_ctx {
     rt::CompiledScene scene;
     float4* d_tri_isect = nullptr;
     float4* d_tri_shade = nullptr;
+    float4* d_pair_isect = nullptr;
     float4* d_sph_isect = nullptr;
     float4* d_sph_shade = nullptr;
     uint32_t* d_seeds = nullptr;
@@ -37,7 +38,7 @@ struct rt_ctx {
     size_t out_cap = 0;     // bytes
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
-    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=lds|smem (tuning knob)
+    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem (tuning knob)
     std::string err;
 };
 
@@ -86,6 +87,7 @@ void release(rt_ctx* c) {
     DeviceGuard g(c->device);
     (void)hipFree(c->d_tri_isect);
     (void)hipFree(c->d_tri_shade);
+    (void)hipFree(c->d_pair_isect);
     (void)hipFree(c->d_sph_isect);
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_seeds);
@@ -168,6 +170,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     memset(&K, 0, sizeof(K));
     K.tri_isect = c->d_tri_isect;
     K.tri_shade = c->d_tri_shade;
+    K.pair_isect = c->d_pair_isect;
     K.sph_isect = c->d_sph_isect;
     K.sph_shade = c->d_sph_shade;
     K.seeds = c->d_seeds;
@@ -175,6 +178,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.out = kout;
     K.nT = (uint32_t)c->scene.tri_isect.size();
     K.nS = (uint32_t)c->scene.sph_isect.size();
+    K.nP = (uint32_t)c->scene.pair_isect.size();
     const rt::CamConst& cam = c->scene.cam;
     memcpy(K.cam_pos, cam.pos, sizeof(K.cam_pos));
     memcpy(K.cam_u, cam.u, sizeof(K.cam_u));
@@ -262,7 +266,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
     c->device = d->device;
     if (const char* m = getenv("RTPT_SCENE_MEM")) {
-        if (!strcmp(m, "lds")) c->scene_mem = rt::SceneMem::kLds;
+        if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
     }
     DeviceGuard g(c->device);
@@ -284,6 +288,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
         const rt::CompiledScene& s = c->scene;
         if ((e = upload(&c->d_tri_isect, s.tri_isect.data(), s.tri_isect.size() * sizeof(rt::TriIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_tri_shade, s.tri_shade.data(), s.tri_shade.size() * sizeof(rt::TriShade), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_pair_isect, s.pair_isect.data(), s.pair_isect.size() * sizeof(rt::PairIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess) {
             status = RT_ERR_OUT_OF_MEMORY; msg = std::string("scene upload: ") + hipGetErrorString(e); break;
@@ -354,6 +359,22 @@ int rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     release(c);
     delete c;
+    return RT_OK;
+}
+
+int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
+    if (!d || !info || !d->camera || !d->square_lights)
+        return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
+    rt::CompiledScene s;
+    const char* err = nullptr;
+    if (!rt::compile_scene(*d->camera, d->materials, d->vertices, d->n_triangles,
+                           d->square_lights[0], d->spheres, d->n_spheres, &s, &err))
+        return fail(nullptr, RT_ERR_INVALID_ARG, err);
+    info->n_triangles = (uint32_t)s.tri_isect.size();
+    info->n_triangle_pairs = (uint32_t)s.pair_isect.size();
+    info->n_spheres = (uint32_t)s.sph_isect.size();
+    const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres);
+    info->lds_bytes = lds <= rt::kMaxLdsBytes ? (uint32_t)lds : 0u;
     return RT_OK;
 }
 

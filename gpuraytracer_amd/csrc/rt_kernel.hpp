@@ -17,13 +17,14 @@ constexpr uint32_t kOutFp16 = 0x2u;
 // Kernel arguments (passed by value -> kernarg segment / SGPRs).
 struct KParams {
     const float4* tri_isect;  // 3 float4 per triangle (TriIsect)
+    const float4* pair_isect; // 5 float4 per shared-edge triangle pair (PairIsect) or null
     const float4* tri_shade;  // 4 float4 per triangle (TriShade)
     const float4* sph_isect;  // 1 float4 per sphere   (SphIsect)
     const float4* sph_shade;  // 2 float4 per sphere   (SphShade)
     const uint32_t* seeds;    // W*H, full frame
     float4* sum;              // running sums (tile layout) or null
     void* out;                // rgba32F / rgba16F tile or null
-    uint32_t nT, nS;
+    uint32_t nT, nP, nS;      // triangles, triangle pairs (0: no pair layout), spheres
     float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
     float halfW, halfH;
     int32_t W, H;
@@ -35,9 +36,9 @@ struct KParams {
     uint32_t flags;
 };
 
-size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_sph);
+size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph);
 // Where the workgroup reads the intersection records from.
-enum class SceneMem { kAuto = 0, kLds = 1, kSmem = 2 };
+enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 

@@ -231,6 +231,40 @@ uint32_t seed_splitmix(uint64_t key, uint64_t p) {
     return (uint32_t)(z & 0xFFFFFu);
 }
 
+static bool same_bits(const float* a, const float* b, int n) {
+    return memcmp(a, b, sizeof(float) * (size_t)n) == 0;
+}
+
+// Pair layout: triangles (2k, 2k+1) with the same v0 and one common edge
+// vector S (bitwise, as computed above).  All-or-nothing, so the kernel keeps
+// testing primitives in id order.
+static void build_pairs(CompiledScene* out) {
+    out->pair_isect.clear();
+    const size_t n = out->tri_isect.size();
+    if (n == 0 || (n & 1)) return;
+    std::vector<PairIsect> pairs(n / 2);
+    for (size_t k = 0; k < n / 2; ++k) {
+        const float* A = out->tri_isect[2 * k].q;      // v0 0..2, e1 3..5, e2 6..8, n 9..11
+        const float* B = out->tri_isect[2 * k + 1].q;
+        if (!same_bits(A, B, 3)) return;
+        const float *S, *eA, *eB;
+        uint32_t m;
+        if (same_bits(A + 3, B + 6, 3)) {         // A.e1 == B.e2
+            S = A + 3; eA = A + 6; eB = B + 3; m = 0u;
+        } else if (same_bits(A + 6, B + 3, 3)) {  // A.e2 == B.e1
+            S = A + 6; eA = A + 3; eB = B + 6; m = 0x80000000u;
+        } else {
+            return;
+        }
+        float mf;
+        memcpy(&mf, &m, 4);
+        const float q[20] = {A[0], A[1], A[2], S[0],  S[1],  S[2],  eA[0], eA[1], eA[2], A[9],
+                             A[10], A[11], eB[0], eB[1], eB[2], B[9], B[10], B[11], mf, 0.0f};
+        memcpy(pairs[k].q, q, sizeof(q));
+    }
+    out->pair_isect.swap(pairs);
+}
+
 static bool finite3(const rt_float3& v) {
     return isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
 }
@@ -302,6 +336,7 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                              em.x, em.y, em.z, mats[k].diffuse.z};
         memcpy(out->tri_shade[k].s, s, sizeof(s));
     }
+    build_pairs(out);
     out->sph_isect.resize(n_sph);
     out->sph_shade.resize(n_sph);
     for (uint32_t k = 0; k < n_sph; ++k) {

@@ -23,6 +23,12 @@ namespace rt {
 struct TriIsect {
     float q[12];
 };
+// Shared-edge triangle pair (2k, 2k+1), 5 x float4 = 80 B, staged in LDS:
+//   r0 = (v0.xyz, S.x)  r1 = (S.yz, eA.xy)  r2 = (eA.z, nA.xyz)
+//   r3 = (eB.xyz, nB.x) r4 = (nB.yz, m, 0)   (see rt_kernel.hip pair_dots)
+struct PairIsect {
+    float q[20];
+};
 // Triangle shading record, 4 x float4 = 64 B, read from global on a hit:
 //   s0 = (N.xyz, light)  s1 = (right.xyz, diffuse.r)
 //   s2 = (fwd.xyz, diffuse.g)  s3 = (emissive.xyz, diffuse.b)
@@ -55,6 +61,7 @@ struct CompiledScene {
     LightConst light;
     std::vector<TriIsect> tri_isect;
     std::vector<TriShade> tri_shade;
+    std::vector<PairIsect> pair_isect;  // empty unless every (2k, 2k+1) shares v0 + an edge
     std::vector<SphIsect> sph_isect;
     std::vector<SphShade> sph_shade;
 };

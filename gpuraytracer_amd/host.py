@@ -18,8 +18,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from ._native import (RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE,
-                      CameraGPU, MaterialGPU, RenderParamsC, RtError, SceneDesc, SphereGPU,
-                      SquareLightGPU, float3, lib)
+                      CameraGPU, MaterialGPU, RenderParamsC, RtError, SceneDesc, SceneInfo,
+                      SphereGPU, SquareLightGPU, float3, lib)
 
 DEFAULT_SEED_KEY = 0x5EED00000000
 
@@ -101,6 +101,12 @@ class Scene:
                                            ctypes.byref(cam), mats, verts, ctypes.byref(light),
                                            ctypes.byref(n), sph))
         return cls(cam, mats, verts, light, sph if n_spheres else None)
+
+    def describe(self) -> dict:
+        """Device layout rt_create would choose (rt_scene_describe)."""
+        info = SceneInfo()
+        _check(lib.rt_scene_describe(ctypes.byref(self.desc()), ctypes.byref(info)))
+        return {k: getattr(info, k) for k, _ in SceneInfo._fields_}
 
     def desc(self, device: int = 0) -> SceneDesc:
         d = SceneDesc()

@@ -144,6 +144,15 @@ int rt_scene_random_spheres(int32_t width, int32_t height, uint32_t n_spheres,
                             rt_float3* vertices, SquareLightGPU* light,
                             uint32_t* n_triangles, SphereGPU* spheres);
 
+/* How rt_create would lay a scene out on the device (host-only, no device). */
+typedef struct rt_scene_info {
+    uint32_t n_triangles;
+    uint32_t n_triangle_pairs;   /* >0: every (2k,2k+1) shares v0 and an edge -> pair records */
+    uint32_t n_spheres;
+    uint32_t lds_bytes;          /* intersection records staged per workgroup (0: read from global) */
+} rt_scene_info;
+int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
+
 /* The reference's image epilogue (RTrace/image.swift:35-65): fp16 round trip,
  * ×2 exposure, Reinhard, gamma 1/2.2, clamp, truncating UInt8, alpha 255.
  * in: n_pixels rgba32F (host), out: n_pixels*4 bytes. */

@@ -72,3 +72,13 @@ def test_no_device_is_reported_loudly():
 def test_seed_helper_range():
     s = g.seed_splitmix(64, 32)
     assert s.shape == (32, 64) and s.dtype == np.uint32 and s.max() < 2**20
+
+
+def test_scene_layout_uses_shared_edge_pairs():
+    info = g.Scene.cornell_box(64, 48).describe()
+    assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
+                    "lds_bytes": 18 * 80}
+    info = g.Scene.random_spheres(64, 48, 1000).describe()
+    assert info["n_triangle_pairs"] == 6 and info["lds_bytes"] == 6 * 80 + 1000 * 16
+    big = g.Scene.random_spheres(16, 8, 5000).describe()
+    assert big["lds_bytes"] == 0  # > 64 KiB: records read from global memory

@@ -158,3 +158,15 @@ def test_errors_are_status_codes():
             r.render(RenderParams(spp=1, row_start=8))
         out = r.render(RenderParams(spp=1))  # context still usable
         assert out.shape == (8, 16, 4)
+
+
+@pytest.mark.parametrize("layout", ["single", "smem"])
+def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
+    """The single-triangle LDS layout and the global (scalar-load) layout give
+    the same bits as the default shared-edge pair layout and the oracle."""
+    monkeypatch.setenv("RTPT_SCENE_MEM", layout)
+    s = Scene.cornell_box(56, 40)
+    sd = seed_splitmix(56, 40, key=99)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=3, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, 3, 3), layout)
