@@ -30,6 +30,7 @@ struct rt_ctx {
     float4* d_sph_shade = nullptr;
     uint32_t* d_seeds = nullptr;
     bool seeds_ready = false;
+    uint32_t seed_max = 0xFFFFFFFFu;  // max seed value (bounds the Halton index)
     float4* d_sum = nullptr;
     size_t sum_cap = 0;  // pixels
     bool sum_valid = false;
@@ -198,6 +199,10 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.accumulate = p->accumulate ? 1u : 0u;
     K.samples_total = (uint32_t)total;
     K.flags = (p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u;
+    {
+        const uint64_t imax = (uint64_t)c->seed_max + p->sample_base + (p->spp ? p->spp - 1u : 0u);
+        K.max_index = imax > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)imax;
+    }
 
     if (keep_sum && !p->accumulate) c->sum_valid = false;  // being overwritten
     (void)hipEventRecord(c->ev0, stream);
@@ -317,6 +322,9 @@ int rt_set_seeds(rt_ctx* c, const uint32_t* seeds, int32_t width, int32_t height
     hipError_t e = hipMemcpyAsync(c->d_seeds, seeds, bytes, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "seed upload", e);
+    uint32_t mx = 0;
+    for (size_t k = 0, n = (size_t)width * (size_t)height; k < n; ++k) mx = seeds[k] > mx ? seeds[k] : mx;
+    c->seed_max = mx;
     c->seeds_ready = true;
     return RT_OK;
 }
@@ -328,6 +336,7 @@ int rt_fill_seeds(rt_ctx* c, uint64_t key) {
     hipError_t e = rt::launch_fill_seeds(c->d_seeds, key, n, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "fill_seeds", e);
+    c->seed_max = 0xFFFFFu;  // splitmix64(.) mod 2^20
     c->seeds_ready = true;
     return RT_OK;
 }

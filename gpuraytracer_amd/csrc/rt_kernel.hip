@@ -40,6 +40,45 @@ __device__ __forceinline__ float halton(uint32_t i) {
     return r;
 }
 
+// Digits of i < 2^bits in base b (compile time).
+constexpr int halton_digits(uint32_t b, int bits) {
+    uint64_t cap = 1;
+    int n = 0;
+    while (cap < (1ull << bits)) {
+        cap *= b;
+        ++n;
+    }
+    return n;
+}
+
+// The same radical inverse for i < 2^21 (every reference seed is < 2^20,
+// renderer.swift:100): the loop runs a fixed digit count, fully unrolled, so
+// f = invB^k folds to compile-time constants and no loop control remains.  The
+// extra iterations past i's last digit add f*0 = +0 to r >= 0: bit-identical.
+constexpr int kSmallIndexBits = 21;
+template <uint32_t D>
+__device__ __forceinline__ float halton_small(uint32_t i) {
+    constexpr uint32_t b = kPrimes[D];
+    constexpr int nd = halton_digits(b, kSmallIndexBits);
+    constexpr float invB = 1.0f / (float)b;
+    float f = 1.0f;
+    float r = 0.0f;
+#pragma unroll
+    for (int k = 0; k < nd; ++k) {
+        f = f * invB;
+        const uint32_t q = i / b;
+        r = r + f * (float)(i - q * b);
+        i = q;
+    }
+    return r;
+}
+
+template <uint32_t D, bool SMALL>
+__device__ __forceinline__ float halton_dim(uint32_t i) {
+    if (SMALL) return halton_small<D>(i);
+    return halton<D>(i);
+}
+
 __device__ __forceinline__ f3 ld_f3(const float* p) { return f3{p[0], p[1], p[2]}; }
 
 // Ray/triangle test of DESIGN.md §3.5 (stands in for Metal's intersector).
@@ -167,18 +206,23 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
             const float4* r = sv.pair + 5 * k;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
             const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
-            if (bary_ok(q.denA, q.a1, q.a2)) {
-                const float t = pair_t(f3{r2.y, r2.z, r2.w}, q.tv, q.denA);
+            const bool pa = bary_ok(q.denA, q.a1, q.a2);
+            const bool pb = bary_ok(q.denB, q.b1, q.b2);
+            if (pa || pb) {
+                // One division for whichever of A, B the ray passes (A first);
+                // a ray on the shared edge passes both and also runs B after.
+                const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+                const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
                 if (t > tmin && t < best) {
                     best = t;
-                    id = (int)(2 * k);
+                    id = (int)(pa ? 2 * k : 2 * k + 1);
                 }
-            }
-            if (bary_ok(q.denB, q.b1, q.b2)) {
-                const float t = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
-                if (t > tmin && t < best) {
-                    best = t;
-                    id = (int)(2 * k + 1);
+                if (pa && pb) {
+                    const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
+                    if (t2 > tmin && t2 < best) {
+                        best = t2;
+                        id = (int)(2 * k + 1);
+                    }
                 }
             }
         }
@@ -215,13 +259,16 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
             const float4* r = sv.pair + 5 * k;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
             const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
-            if (bary_ok(q.denA, q.a1, q.a2)) {
-                const float t = pair_t(f3{r2.y, r2.z, r2.w}, q.tv, q.denA);
+            const bool pa = bary_ok(q.denA, q.a1, q.a2);
+            const bool pb = bary_ok(q.denB, q.b1, q.b2);
+            if (pa || pb) {
+                const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+                const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
                 if (t > tmin && t < tmax) return true;
-            }
-            if (bary_ok(q.denB, q.b1, q.b2)) {
-                const float t = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
-                if (t > tmin && t < tmax) return true;
+                if (pa && pb) {
+                    const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
+                    if (t2 > tmin && t2 < tmax) return true;
+                }
             }
         }
     } else {
@@ -248,7 +295,7 @@ struct PathState {
 };
 
 // One bounce b of raytrace.metal:47-101.  Returns false when the path ends.
-template <int b, int B, int GEO, bool SPH>
+template <int b, int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, PathState& s) {
     float t = 1000.0f;                                      // max_distance (sampling.metal:155)
     const int id = closest_hit<GEO, SPH>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
@@ -284,8 +331,8 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     const f3 p = (s.o + s.d * t) + N * 1e-3f;              // :67
 
     // sampleAreaLight (sampling.metal:198-236), dims 2+5b, 3+5b (:72-74)
-    const float ux = halton<2 + 5 * b>(s.i) * 2.0f - 1.0f;
-    const float uy = halton<3 + 5 * b>(s.i) * 2.0f - 1.0f;
+    const float ux = halton_dim<2 + 5 * b, SMALL>(s.i) * 2.0f - 1.0f;
+    const float uy = halton_dim<3 + 5 * b, SMALL>(s.i) * 2.0f - 1.0f;
     const f3 lcen = ld_f3(P.light_center);
     const f3 q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
     f3 L = q - p;
@@ -299,8 +346,8 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     if (!any_hit<GEO, SPH>(sv, p, L, 0.0f, dist - 1e-3f))       // :79-85
         s.acc = s.acc + lc * s.thr;                        // :87-89
     if (b + 1 < B) {                                       // last direction never traced
-        const float cu = halton<4 + 5 * b>(s.i);           // :93-94
-        const float cv = halton<5 + 5 * b>(s.i);
+        const float cu = halton_dim<4 + 5 * b, SMALL>(s.i);           // :93-94
+        const float cv = halton_dim<5 + 5 * b, SMALL>(s.i);
         float sp, cp;
         sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
         const float ct = sqrtf(cv);
@@ -311,22 +358,22 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     return true;
 }
 
-template <int b, int B, int GEO, bool SPH>
+template <int b, int B, int GEO, bool SPH, bool SMALL>
 struct BounceChain {
     __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv,
                                                PathState& s) {
-        if (!bounce<b, B, GEO, SPH>(P, sv, s)) return;
-        BounceChain<b + 1, B, GEO, SPH>::run(P, sv, s);
+        if (!bounce<b, B, GEO, SPH, SMALL>(P, sv, s)) return;
+        BounceChain<b + 1, B, GEO, SPH, SMALL>::run(P, sv, s);
     }
 };
-template <int B, int GEO, bool SPH>
-struct BounceChain<B, B, GEO, SPH> {
+template <int B, int GEO, bool SPH, bool SMALL>
+struct BounceChain<B, B, GEO, SPH, SMALL> {
     __device__ __forceinline__ static void run(const KParams&, const SceneView&, PathState&) {}
 };
 
 }  // namespace
 
-template <int B, int GEO, bool SPH>
+template <int B, int GEO, bool SPH, bool SMALL>
 __global__ __launch_bounds__(kBlockThreads) void path_trace_kernel(KParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
@@ -369,7 +416,7 @@ __global__ __launch_bounds__(kBlockThreads) void path_trace_kernel(KParams P) {
     for (uint32_t n = 0; n < P.spp; ++n) {                       // :34
         PathState s;
         s.i = seed + (P.sample_base + n);
-        const float jx = halton<0>(s.i), jy = halton<1>(s.i);   // :39-40
+        const float jx = halton_dim<0, SMALL>(s.i), jy = halton_dim<1, SMALL>(s.i);   // :39-40
         // generateCameraRay (sampling.metal:125-157)
         const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
         const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
@@ -378,7 +425,7 @@ __global__ __launch_bounds__(kBlockThreads) void path_trace_kernel(KParams P) {
         s.o = ld_f3(P.cam_pos);
         s.acc = f3{0.0f, 0.0f, 0.0f};
         s.thr = f3{1.0f, 1.0f, 1.0f};
-        BounceChain<0, B, GEO, SPH>::run(P, sv, s);                  // :47-102
+        BounceChain<0, B, GEO, SPH, SMALL>::run(P, sv, s);                  // :47-102
         lum = lum + s.acc;                                       // :103
     }
     if (P.sum) P.sum[o] = make_float4(lum.x, lum.y, lum.z, (float)P.samples_total);
@@ -411,18 +458,22 @@ __global__ void fill_seeds_kernel(uint32_t* seeds, uint64_t key, uint64_t n) {
 
 namespace {
 
-template <int B, int GEO, bool SPH>
+template <int B, int GEO, bool SPH, bool SMALL>
 hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
-    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH>), grid, dim3(kBlockThreads),
+    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(kBlockThreads),
                        GEO == kGeoTriGlobal ? 0 : lds_bytes, stream, P);
     return hipGetLastError();
 }
 
 template <int B, int GEO>
 hipError_t launch_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
-    return P.nS > 0 ? launch_t<B, GEO, true>(P, lds_bytes, stream)
-                    : launch_t<B, GEO, false>(P, lds_bytes, stream);
+    const bool small = P.max_index < (1u << kSmallIndexBits);
+    if (P.nS > 0)
+        return small ? launch_t<B, GEO, true, true>(P, lds_bytes, stream)
+                     : launch_t<B, GEO, true, false>(P, lds_bytes, stream);
+    return small ? launch_t<B, GEO, false, true>(P, lds_bytes, stream)
+                 : launch_t<B, GEO, false, false>(P, lds_bytes, stream);
 }
 
 template <int B>

@@ -34,6 +34,7 @@ struct KParams {
     uint32_t accumulate;      // read P.sum before adding
     uint32_t samples_total;   // S of `luminance /= samples`
     uint32_t flags;
+    uint32_t max_index;       // max Halton index seed+n of this launch (0xFFFFFFFF: unknown/wraps)
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph);
