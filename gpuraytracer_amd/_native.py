@@ -12,7 +12,8 @@ import os
 
 ABI_VERSION = 1
 _HERE = os.path.dirname(os.path.abspath(__file__))
-library_path = os.path.join(_HERE, "librtpt.so")
+# RTPT_LIB overrides the in-tree library (A/B builds of the kernel).
+library_path = os.environ.get("RTPT_LIB") or os.path.join(_HERE, "librtpt.so")
 
 
 class float3(ctypes.Structure):
