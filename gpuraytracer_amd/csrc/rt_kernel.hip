@@ -203,7 +203,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
     int id = -1;
     if (GEO == kGeoPairLds) {
         for (uint32_t k = 0; k < sv.nP; ++k) {
-            const float4* r = sv.pair + 5 * k;
+            const float4* r = sv.pair + kPairF4 * k;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
             const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
             const bool pa = bary_ok(q.denA, q.a1, q.a2);
@@ -252,11 +252,19 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
 
 // any hit, accept_any_intersection(true) (raytrace.metal:79-85).  The boolean
 // result does not depend on the order of the tests.
+// seg_lo/seg_hi bound every point the ray can accept (t in (tmin, tmax)); a
+// pair whose padded AABB no lane's segment box touches cannot be hit by any
+// lane of the wave and is skipped as a whole.
 template <int GEO, bool SPH>
-__device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax) {
+__device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
+                                        f3 seg_lo, f3 seg_hi) {
     if (GEO == kGeoPairLds) {
         for (uint32_t k = 0; k < sv.nP; ++k) {
-            const float4* r = sv.pair + 5 * k;
+            const float4* r = sv.pair + kPairF4 * k;
+            const float4 b0 = r[5], b1 = r[6];
+            const bool overlap = seg_lo.x <= b0.w && seg_hi.x >= b0.x && seg_lo.y <= b1.x &&
+                                 seg_hi.y >= b0.y && seg_lo.z <= b1.y && seg_hi.z >= b0.z;
+            if (!__any(overlap)) continue;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
             const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
             const bool pa = bary_ok(q.denA, q.a1, q.a2);
@@ -343,7 +351,9 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     lc = lc * saturate(dot(-L, f3{0.0f, -1.0f, 0.0f}));
     lc = lc * saturate(dot(N, L));                         // :75
     s.thr = s.thr * diffuse;                               // :76
-    if (!any_hit<GEO, SPH>(sv, p, L, 0.0f, dist - 1e-3f))       // :79-85
+    const f3 seg_lo{fminf(p.x, q.x), fminf(p.y, q.y), fminf(p.z, q.z)};
+    const f3 seg_hi{fmaxf(p.x, q.x), fmaxf(p.y, q.y), fmaxf(p.z, q.z)};
+    if (!any_hit<GEO, SPH>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + lc * s.thr;                        // :87-89
     if (b + 1 < B) {                                       // last direction never traced
         const float cu = halton_dim<4 + 5 * b, SMALL>(s.i);           // :93-94
@@ -385,7 +395,7 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
     sv.nS = SPH ? P.nS : 0u;
     if (GEO != kGeoTriGlobal) {
         // Stage the intersection records once per workgroup.
-        const uint32_t ng4 = (GEO == kGeoPairLds) ? 5u * sv.nP : 3u * sv.nT;
+        const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
         if (SPH)
@@ -491,7 +501,7 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
 }  // namespace
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph) {
-    const uint32_t geo4 = n_pairs ? 5u * n_pairs : 3u * n_tri;
+    const uint32_t geo4 = n_pairs ? kPairF4 * n_pairs : 3u * n_tri;
     return (size_t)(geo4 + n_sph) * sizeof(float4);
 }
 

@@ -13,11 +13,12 @@ constexpr uint32_t kBlockThreads = 256;  // 4 waves; each wave = 8x8 pixel tile
 constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
 constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
+constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
 
 // Kernel arguments (passed by value -> kernarg segment / SGPRs).
 struct KParams {
     const float4* tri_isect;  // 3 float4 per triangle (TriIsect)
-    const float4* pair_isect; // 5 float4 per shared-edge triangle pair (PairIsect) or null
+    const float4* pair_isect; // kPairF4 float4 per shared-edge triangle pair (PairIsect) or null
     const float4* tri_shade;  // 4 float4 per triangle (TriShade)
     const float4* sph_isect;  // 1 float4 per sphere   (SphIsect)
     const float4* sph_shade;  // 2 float4 per sphere   (SphShade)

@@ -235,13 +235,24 @@ static bool same_bits(const float* a, const float* b, int n) {
     return memcmp(a, b, sizeof(float) * (size_t)n) == 0;
 }
 
+// Conservative culling margin: far above the fp32 rounding of the triangle
+// test at the scene's scale (~1e-6 relative), far below the 1e-3 surface
+// offset of raytrace.metal:67.
+static float culling_margin(const rt_float3* verts, uint32_t n_tri) {
+    float ext = 2.5f;
+    for (uint32_t k = 0; k < 3 * n_tri; ++k)
+        ext = fmaxf(ext, fmaxf(fabsf(verts[k].x), fmaxf(fabsf(verts[k].y), fabsf(verts[k].z))));
+    return 4e-5f * ext;
+}
+
 // Pair layout: triangles (2k, 2k+1) with the same v0 and one common edge
 // vector S (bitwise, as computed above).  All-or-nothing, so the kernel keeps
 // testing primitives in id order.
-static void build_pairs(CompiledScene* out) {
+static void build_pairs(CompiledScene* out, const rt_float3* verts) {
     out->pair_isect.clear();
     const size_t n = out->tri_isect.size();
     if (n == 0 || (n & 1)) return;
+    const float margin = culling_margin(verts, (uint32_t)n);
     std::vector<PairIsect> pairs(n / 2);
     for (size_t k = 0; k < n / 2; ++k) {
         const float* A = out->tri_isect[2 * k].q;      // v0 0..2, e1 3..5, e2 6..8, n 9..11
@@ -258,8 +269,21 @@ static void build_pairs(CompiledScene* out) {
         }
         float mf;
         memcpy(&mf, &m, 4);
-        const float q[20] = {A[0], A[1], A[2], S[0],  S[1],  S[2],  eA[0], eA[1], eA[2], A[9],
-                             A[10], A[11], eB[0], eB[1], eB[2], B[9], B[10], B[11], mf, 0.0f};
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t v = 6 * k; v < 6 * k + 6; ++v) {
+            const float c[3] = {verts[v].x, verts[v].y, verts[v].z};
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = fminf(lo[a], c[a]);
+                hi[a] = fmaxf(hi[a], c[a]);
+            }
+        }
+        for (int a = 0; a < 3; ++a) {
+            lo[a] -= margin;
+            hi[a] += margin;
+        }
+        const float q[28] = {A[0],  A[1],  A[2],  S[0],  S[1],  S[2],  eA[0], eA[1], eA[2], A[9],
+                             A[10], A[11], eB[0], eB[1], eB[2], B[9],  B[10], B[11], mf,    0.0f,
+                             lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], 0.0f,  0.0f};
         memcpy(pairs[k].q, q, sizeof(q));
     }
     out->pair_isect.swap(pairs);
@@ -336,7 +360,7 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                              em.x, em.y, em.z, mats[k].diffuse.z};
         memcpy(out->tri_shade[k].s, s, sizeof(s));
     }
-    build_pairs(out);
+    build_pairs(out, verts);
     out->sph_isect.resize(n_sph);
     out->sph_shade.resize(n_sph);
     for (uint32_t k = 0; k < n_sph; ++k) {

@@ -23,11 +23,13 @@ namespace rt {
 struct TriIsect {
     float q[12];
 };
-// Shared-edge triangle pair (2k, 2k+1), 5 x float4 = 80 B, staged in LDS:
+// Shared-edge triangle pair (2k, 2k+1), 7 x float4 = 112 B, staged in LDS:
 //   r0 = (v0.xyz, S.x)  r1 = (S.yz, eA.xy)  r2 = (eA.z, nA.xyz)
 //   r3 = (eB.xyz, nB.x) r4 = (nB.yz, m, 0)   (see rt_kernel.hip pair_dots)
+//   r5 = (lo.xyz, hi.x) r6 = (hi.yz, 0, 0)   AABB of both triangles, padded by
+//   the culling margin
 struct PairIsect {
-    float q[20];
+    float q[28];
 };
 // Triangle shading record, 4 x float4 = 64 B, read from global on a hit:
 //   s0 = (N.xyz, light)  s1 = (right.xyz, diffuse.r)

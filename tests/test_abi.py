@@ -77,8 +77,8 @@ def test_seed_helper_range():
 def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.cornell_box(64, 48).describe()
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
-                    "lds_bytes": 18 * 80}
+                    "lds_bytes": 18 * 112}
     info = g.Scene.random_spheres(64, 48, 1000).describe()
-    assert info["n_triangle_pairs"] == 6 and info["lds_bytes"] == 6 * 80 + 1000 * 16
+    assert info["n_triangle_pairs"] == 6 and info["lds_bytes"] == 6 * 112 + 1000 * 16
     big = g.Scene.random_spheres(16, 8, 5000).describe()
     assert big["lds_bytes"] == 0  # > 64 KiB: records read from global memory

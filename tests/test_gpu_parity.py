@@ -170,3 +170,41 @@ def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
     with Renderer(s, seeds=sd) as r:
         out = r.render(RenderParams(spp=3, bounces=3))
     assert_parity(out, oracle_lib.render(s, sd, 3, 3), layout)
+
+
+def random_quad_scene(w, h, n_quads, seed):
+    """Cornell camera/light + random planar-ish quads as shared-edge pairs:
+    stresses the pair layout and the conservative segment culling."""
+    base = Scene.cornell_box(w, h)
+    rng = np.random.default_rng(seed)
+    n = 2 * n_quads + 2
+    mats = (MaterialGPU * n)()
+    verts = (float3 * (3 * n))()
+    for q in range(n_quads):
+        c = rng.uniform(-2.2, 2.2, 3)
+        a, b = rng.normal(size=3), rng.normal(size=3)
+        a *= rng.uniform(0.05, 1.5) / np.linalg.norm(a)
+        b *= rng.uniform(0.05, 1.5) / np.linalg.norm(b)
+        P = [c, c + a, c + a + b, c + b]
+        for t, tri in enumerate([(P[0], P[1], P[2]), (P[0], P[2], P[3])]):
+            k = 2 * q + t
+            for v in range(3):
+                verts[3 * k + v].x, verts[3 * k + v].y, verts[3 * k + v].z = (float(x) for x in tri[v])
+            col = rng.uniform(0.1, 0.9, 3)
+            mats[k].diffuse.x, mats[k].diffuse.y, mats[k].diffuse.z, mats[k].diffuse.w = (*col, 1.0)
+    for t in range(2):  # keep the emissive light pair (ids 34, 35 of the Cornell scene)
+        k = 2 * n_quads + t
+        mats[k] = base.materials[34 + t]
+        for v in range(3):
+            verts[3 * k + v] = base.vertices[3 * (34 + t) + v]
+    return Scene(base.camera, mats, verts, base.light)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_quads_pair_layout_and_culling_bit_exact(seed):
+    s = random_quad_scene(48, 32, 25, seed)
+    assert s.describe()["n_triangle_pairs"] == 26
+    sd = seed_splitmix(48, 32, key=seed)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=16, bounces=4))
+    assert_parity(out, oracle_lib.render(s, sd, 16, 4), f"quads seed {seed}")
