@@ -196,14 +196,29 @@ struct SceneView {
 // closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
 // Primitives are tested in id order; a strictly smaller t wins (ties keep the
 // lower id), exactly as the oracle.
-template <int GEO, bool SPH>
+// With CULL (used for coherent camera rays) a pair is skipped when no lane's
+// box around its current candidate segment [o, o + d*best] touches the pair's
+// padded AABB: any hit that could still win has t < best and lies inside it.
+template <int GEO, bool SPH, bool CULL>
 __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, float tmin,
                                            float* t_io) {
     float best = *t_io;
     int id = -1;
     if (GEO == kGeoPairLds) {
+        f3 seg_lo, seg_hi;
+        if (CULL) {
+            const f3 e = o + d * best;
+            seg_lo = f3{fminf(o.x, e.x), fminf(o.y, e.y), fminf(o.z, e.z)};
+            seg_hi = f3{fmaxf(o.x, e.x), fmaxf(o.y, e.y), fmaxf(o.z, e.z)};
+        }
         for (uint32_t k = 0; k < sv.nP; ++k) {
             const float4* r = sv.pair + kPairF4 * k;
+            if (CULL) {
+                const float4 b0 = r[5], b1 = r[6];
+                const bool overlap = seg_lo.x <= b0.w && seg_hi.x >= b0.x && seg_lo.y <= b1.x &&
+                                     seg_hi.y >= b0.y && seg_lo.z <= b1.y && seg_hi.z >= b0.z;
+                if (!__any(overlap)) continue;
+            }
             const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
             const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
             const bool pa = bary_ok(q.denA, q.a1, q.a2);
@@ -223,6 +238,11 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
                         best = t2;
                         id = (int)(2 * k + 1);
                     }
+                }
+                if (CULL) {
+                    const f3 e = o + d * best;
+                    seg_lo = f3{fminf(o.x, e.x), fminf(o.y, e.y), fminf(o.z, e.z)};
+                    seg_hi = f3{fmaxf(o.x, e.x), fmaxf(o.y, e.y), fmaxf(o.z, e.z)};
                 }
             }
         }
@@ -306,7 +326,7 @@ struct PathState {
 template <int b, int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, PathState& s) {
     float t = 1000.0f;                                      // max_distance (sampling.metal:155)
-    const int id = closest_hit<GEO, SPH>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
+    const int id = closest_hit<GEO, SPH, b == 0>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
     if (id < 0) return false;                               // :51-53
     f3 N, right, fwd, diffuse;
     if (!SPH || (uint32_t)id < sv.nT) {
