@@ -105,6 +105,7 @@ SIGNATURES = {
     "rt_render_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),
     "rt_last_kernel_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_destroy": (ctypes.c_int, [_P]),
+    "rt_debug_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "rt_last_error": (ctypes.c_char_p, [_P]),
     "rt_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "rt_abi_version": (ctypes.c_int, []),

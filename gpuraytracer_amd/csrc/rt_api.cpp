@@ -39,7 +39,7 @@ struct rt_ctx {
     size_t out_cap = 0;     // bytes
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
-    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem (tuning knob)
+    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|sorted (tuning knob)
     std::string err;
 };
 
@@ -273,6 +273,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     if (const char* m = getenv("RTPT_SCENE_MEM")) {
         if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
+        if (!strcmp(m, "sorted")) c->scene_mem = rt::SceneMem::kPairSorted;
     }
     DeviceGuard g(c->device);
     const char* err = nullptr;
@@ -384,6 +385,15 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     info->n_spheres = (uint32_t)s.sph_isect.size();
     const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres);
     info->lds_bytes = lds <= rt::kMaxLdsBytes ? (uint32_t)lds : 0u;
+    return RT_OK;
+}
+
+int rt_debug_stats(rt_ctx* c, uint64_t* out, int n) {
+    if (!c || !out || n <= 0) return fail(c, RT_ERR_INVALID_ARG, "null argument");
+    DeviceGuard g(c->device);
+    hipError_t e = rt::read_debug_stats(reinterpret_cast<unsigned long long*>(out), n);
+    if (e == hipErrorNotSupported) return fail(c, RT_ERR_STATE, "not an RT_STATS build");
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "read stats", e);
     return RT_OK;
 }
 

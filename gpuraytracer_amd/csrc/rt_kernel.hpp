@@ -40,8 +40,9 @@ struct KParams {
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph);
 // Where the workgroup reads the intersection records from.
-enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2 };
+enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
+hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 
 }  // namespace rt

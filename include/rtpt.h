@@ -116,6 +116,10 @@ int rt_last_kernel_ms(rt_ctx* ctx, float* ms);
 
 int rt_destroy(rt_ctx* ctx);
 
+/* Diagnostic counters of a -DRT_STATS build of the kernel (reads and clears
+ * up to 16 uint64 counters; RT_ERR_STATE in normal builds). */
+int rt_debug_stats(rt_ctx* ctx, uint64_t* out, int n);
+
 /* Message of the last failure on ctx (or of the last failed rt_create when
  * ctx is NULL).  Never NULL. */
 const char* rt_last_error(const rt_ctx* ctx);

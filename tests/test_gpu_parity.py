@@ -160,10 +160,11 @@ def test_errors_are_status_codes():
         assert out.shape == (8, 16, 4)
 
 
-@pytest.mark.parametrize("layout", ["single", "smem"])
+@pytest.mark.parametrize("layout", ["single", "smem", "sorted"])
 def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
-    """The single-triangle LDS layout and the global (scalar-load) layout give
-    the same bits as the default shared-edge pair layout and the oracle."""
+    """The single-triangle LDS layout, the global (scalar-load) layout and the
+    octant-sorted path kernel give the same bits as the default pair kernel
+    and the oracle."""
     monkeypatch.setenv("RTPT_SCENE_MEM", layout)
     s = Scene.cornell_box(56, 40)
     sd = seed_splitmix(56, 40, key=99)
