@@ -257,3 +257,19 @@ def test_tonemap_matches_image_swift():
     a, b = tonemap_rgba8(x), oracle_lib.tonemap(x)
     assert np.array_equal(a, b)
     assert list(a[0]) == [0, 212, 255, 255]  # 1.0 -> (2/3)^(1/2.2)*255 = 212
+
+
+def test_halton_small_magic_table():
+    """The kernel's 24-bit magic division (rt_kernel.hip kMagicM/kMagicS) is
+    exact for every index < 2^21, for all 24 Halton bases."""
+    import re
+    src = open(os.path.join(os.path.dirname(GOLDEN), "..", "gpuraytracer_amd", "csrc",
+                            "rt_kernel.hip")).read()
+    M = [int(v) for v in re.search(r"kMagicM\[24\] = \{([^}]*)\}", src).group(1).split(",")]
+    S = [int(v) for v in re.search(r"kMagicS\[24\] = \{([^}]*)\}", src).group(1).split(",")]
+    primes = [2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73,
+              79, 83, 89]
+    i = np.arange(1 << 21, dtype=np.uint64)
+    for b, m, s in zip(primes, M, S):
+        assert m < (1 << 24) and s < 32
+        assert np.array_equal((i * np.uint64(m)) >> np.uint64(s), i // np.uint64(b)), b
