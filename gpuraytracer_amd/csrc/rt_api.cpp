@@ -28,6 +28,8 @@ struct rt_ctx {
     float4* d_pair_isect = nullptr;
     float4* d_sph_isect = nullptr;
     float4* d_sph_shade = nullptr;
+    float4* d_sph_nodes = nullptr;
+    uint32_t* d_sph_perm = nullptr;
     uint32_t* d_seeds = nullptr;
     bool seeds_ready = false;
     uint32_t seed_max = 0xFFFFFFFFu;  // max seed value (bounds the Halton index)
@@ -91,6 +93,8 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_pair_isect);
     (void)hipFree(c->d_sph_isect);
     (void)hipFree(c->d_sph_shade);
+    (void)hipFree(c->d_sph_nodes);
+    (void)hipFree(c->d_sph_perm);
     (void)hipFree(c->d_seeds);
     (void)hipFree(c->d_sum);
     (void)hipFree(c->d_out);
@@ -174,12 +178,15 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.pair_isect = c->d_pair_isect;
     K.sph_isect = c->d_sph_isect;
     K.sph_shade = c->d_sph_shade;
+    K.sph_nodes = c->d_sph_nodes;
+    K.sph_perm = c->d_sph_perm;
     K.seeds = c->d_seeds;
     K.sum = (keep_sum || p->accumulate) ? c->d_sum : nullptr;
     K.out = kout;
     K.nT = (uint32_t)c->scene.tri_isect.size();
     K.nS = (uint32_t)c->scene.sph_isect.size();
     K.nP = (uint32_t)c->scene.pair_isect.size();
+    K.nN = (uint32_t)c->scene.sph_nodes.size();
     const rt::CamConst& cam = c->scene.cam;
     memcpy(K.cam_pos, cam.pos, sizeof(K.cam_pos));
     memcpy(K.cam_u, cam.u, sizeof(K.cam_u));
@@ -296,7 +303,9 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
             (e = upload(&c->d_tri_shade, s.tri_shade.data(), s.tri_shade.size() * sizeof(rt::TriShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_pair_isect, s.pair_isect.data(), s.pair_isect.size() * sizeof(rt::PairIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
-            (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess) {
+            (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_nodes, s.sph_nodes.data(), s.sph_nodes.size() * sizeof(rt::BvhNode), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_perm, s.sph_perm.data(), s.sph_perm.size() * sizeof(uint32_t), c->stream)) != hipSuccess) {
             status = RT_ERR_OUT_OF_MEMORY; msg = std::string("scene upload: ") + hipGetErrorString(e); break;
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
@@ -383,7 +392,9 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     info->n_triangles = (uint32_t)s.tri_isect.size();
     info->n_triangle_pairs = (uint32_t)s.pair_isect.size();
     info->n_spheres = (uint32_t)s.sph_isect.size();
-    const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres);
+    info->n_sphere_nodes = (uint32_t)s.sph_nodes.size();
+    const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres,
+                                            (uint32_t)s.sph_nodes.size());
     info->lds_bytes = lds <= rt::kMaxLdsBytes ? (uint32_t)lds : 0u;
     return RT_OK;
 }

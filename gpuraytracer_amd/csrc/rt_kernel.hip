@@ -232,11 +232,42 @@ enum Geo : int {
 };
 
 struct SceneView {
-    const float4* tri;   // 3 float4 per triangle (single layout)
-    const float4* pair;  // 5 float4 per triangle pair (pair layout)
-    const float4* sph;   // 1 float4 per sphere
-    uint32_t nT, nP, nS;
+    const float4* tri;        // 3 float4 per triangle (single layout)
+    const float4* pair;       // kPairF4 float4 per triangle pair (pair layout)
+    const float4* sph;        // 1 float4 per sphere, BVH leaf order
+    const float4* node;       // 2 float4 per sphere-BVH node
+    const uint32_t* sph_perm; // leaf order -> sphere id (global memory)
+    uint32_t nT, nP, nS, nN;
 };
+
+// Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
+// node boxes carry the culling margin, so only speed depends on its rounding.
+struct RayBox {
+    f3 invd, oinv;
+};
+
+__device__ __forceinline__ float safe_rcp(float v) {
+    return __builtin_amdgcn_rcpf(fabsf(v) < 1e-20f ? copysignf(1e-20f, v) : v);
+}
+
+__device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
+    RayBox r;
+    r.invd = f3{safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z)};
+    r.oinv = f3{o.x * r.invd.x, o.y * r.invd.y, o.z * r.invd.z};
+    return r;
+}
+
+// Conservative ray/box overlap on (tmin, tmax): false only if no point of the
+// padded box lies on the ray inside that range.
+__device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, const RayBox& rb,
+                                         float tmin, float tmax) {
+    const float tx0 = fmaf(n0.x, rb.invd.x, -rb.oinv.x), tx1 = fmaf(n1.x, rb.invd.x, -rb.oinv.x);
+    const float ty0 = fmaf(n0.y, rb.invd.y, -rb.oinv.y), ty1 = fmaf(n1.y, rb.invd.y, -rb.oinv.y);
+    const float tz0 = fmaf(n0.z, rb.invd.z, -rb.oinv.z), tz1 = fmaf(n1.z, rb.invd.z, -rb.oinv.z);
+    const float tnear = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+    const float tfar = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    return tnear <= tfar;
+}
 
 // closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
 // Primitives are tested in id order; a strictly smaller t wins (ties keep the
@@ -306,13 +337,35 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
         }
     }
     if (SPH) {
+        // Stackless depth-first walk of the sphere BVH (escape indices).  A
+        // node is skipped only if its padded box has no point on the ray in
+        // (tmin, best]; candidates are ranked by (t, sphere id) exactly like
+        // the oracle's id-ordered scan with strict '<'.
         const float a = dot(d, d);
-        for (uint32_t k = 0; k < sv.nS; ++k) {
-            float t;
-            if (sph_test(sv.sph[k], o, d, a, tmin, best, &t)) {
-                best = t;
-                id = (int)(sv.nT + k);
+        const RayBox rb = ray_box(o, d);
+        uint32_t idx = 0;
+        while (idx < sv.nN) {
+            const float4 n0 = sv.node[2 * idx], n1 = sv.node[2 * idx + 1];
+            uint32_t next = __float_as_uint(n0.w);
+            if (node_hit(n0, n1, rb, tmin, best)) {
+                const uint32_t leaf = __float_as_uint(n1.w);
+                if (leaf == 0u) {
+                    next = idx + 1;
+                } else {
+                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                    for (uint32_t k = first; k < end; ++k) {
+                        float t;
+                        if (sph_test(sv.sph[k], o, d, a, tmin, 3.0e38f, &t) && t <= best) {
+                            const int sid = (int)(sv.nT + sv.sph_perm[k]);
+                            if (t < best || sid < id) {
+                                best = t;
+                                id = sid;
+                            }
+                        }
+                    }
+                }
             }
+            idx = next;
         }
     }
     *t_io = best;
@@ -362,9 +415,24 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
     }
     if (SPH) {
         const float a = dot(d, d);
-        for (uint32_t k = 0; k < sv.nS; ++k) {
-            float t;
-            if (sph_test(sv.sph[k], o, d, a, tmin, tmax, &t)) return true;
+        const RayBox rb = ray_box(o, d);
+        uint32_t idx = 0;
+        while (idx < sv.nN) {
+            const float4 n0 = sv.node[2 * idx], n1 = sv.node[2 * idx + 1];
+            uint32_t next = __float_as_uint(n0.w);
+            if (node_hit(n0, n1, rb, tmin, tmax)) {
+                const uint32_t leaf = __float_as_uint(n1.w);
+                if (leaf == 0u) {
+                    next = idx + 1;
+                } else {
+                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                    for (uint32_t k = first; k < end; ++k) {
+                        float t;
+                        if (sph_test(sv.sph[k], o, d, a, tmin, tmax, &t)) return true;
+                    }
+                }
+            }
+            idx = next;
         }
     }
     return false;
@@ -397,14 +465,14 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         diffuse = f3{s1.w, s2.w, s3.w};
     } else {
         const uint32_t k = (uint32_t)id - sv.nT;
-        const float4* sh = P.sph_shade + 2 * k;
+        const float4* sh = P.sph_shade + 3 * k;
         const float4 s0 = sh[0];
         if (s0.w != 0.0f) {
             const float4 s1 = sh[1];
             s.acc = f3{s1.x, s1.y, s1.z};
             return false;
         }
-        const float4 S = sv.sph[k];
+        const float4 S = sh[2];
         N = normalize((s.o + s.d * t) - f3{S.x, S.y, S.z});
         shading_frame(N, &right, &fwd);
         diffuse = f3{s0.x, s0.y, s0.z};
@@ -600,18 +668,26 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
         const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
-        if (SPH)
+        if (SPH) {
+            const uint32_t nn4 = 2u * P.nN;
+            for (uint32_t k = threadIdx.x; k < nn4; k += kBlockThreads)
+                lds[ng4 + k] = P.sph_nodes[k];
             for (uint32_t k = threadIdx.x; k < sv.nS; k += kBlockThreads)
-                lds[ng4 + k] = P.sph_isect[k];
+                lds[ng4 + nn4 + k] = P.sph_isect[k];
+        }
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
-        sv.sph = lds + ng4;
+        sv.node = lds + ng4;
+        sv.sph = lds + ng4 + 2u * P.nN;
     } else {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
+        sv.node = P.sph_nodes;
         sv.sph = P.sph_isect;
     }
+    sv.nN = SPH ? P.nN : 0u;
+    sv.sph_perm = P.sph_perm;
 
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
@@ -671,11 +747,17 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
     const uint32_t ng4 = kPairF4 * sv.nP;
     float4* scene = lds + kSortF4;  // sort buffers first: compile-time offsets
     for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) scene[k] = P.pair_isect[k];
-    if (SPH)
-        for (uint32_t k = threadIdx.x; k < sv.nS; k += kBlockThreads) scene[ng4 + k] = P.sph_isect[k];
+    sv.nN = SPH ? P.nN : 0u;
+    if (SPH) {
+        for (uint32_t k = threadIdx.x; k < 2u * sv.nN; k += kBlockThreads) scene[ng4 + k] = P.sph_nodes[k];
+        for (uint32_t k = threadIdx.x; k < sv.nS; k += kBlockThreads)
+            scene[ng4 + 2u * sv.nN + k] = P.sph_isect[k];
+    }
     sv.tri = scene;
     sv.pair = scene;
-    sv.sph = scene + ng4;
+    sv.node = scene + ng4;
+    sv.sph = scene + ng4 + 2u * sv.nN;
+    sv.sph_perm = P.sph_perm;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
@@ -793,15 +875,15 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
 
 }  // namespace
 
-size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph) {
+size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes) {
     const uint32_t geo4 = n_pairs ? kPairF4 * n_pairs : 3u * n_tri;
-    return (size_t)(geo4 + n_sph) * sizeof(float4);
+    return (size_t)(geo4 + 2u * n_nodes + n_sph) * sizeof(float4);
 }
 
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
                              hipStream_t stream) {
     const bool pairs = P.nP > 0 && mem != SceneMem::kLdsSingle;
-    const size_t lds_bytes = kernel_lds_bytes(P.nT, pairs ? P.nP : 0u, P.nS);
+    const size_t lds_bytes = kernel_lds_bytes(P.nT, pairs ? P.nP : 0u, P.nS, P.nN);
     int geo = kGeoTriGlobal;
     if (mem != SceneMem::kSmem && lds_bytes <= kMaxLdsBytes) geo = pairs ? kGeoPairLds : kGeoTriLds;
     // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the

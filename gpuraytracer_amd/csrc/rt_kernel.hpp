@@ -20,12 +20,14 @@ struct KParams {
     const float4* tri_isect;  // 3 float4 per triangle (TriIsect)
     const float4* pair_isect; // kPairF4 float4 per shared-edge triangle pair (PairIsect) or null
     const float4* tri_shade;  // 4 float4 per triangle (TriShade)
-    const float4* sph_isect;  // 1 float4 per sphere   (SphIsect)
-    const float4* sph_shade;  // 2 float4 per sphere   (SphShade)
+    const float4* sph_isect;  // 1 float4 per sphere, BVH leaf order (SphIsect)
+    const float4* sph_nodes;  // 2 float4 per sphere-BVH node (BvhNode)
+    const uint32_t* sph_perm; // BVH leaf order -> sphere id
+    const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
     const uint32_t* seeds;    // W*H, full frame
     float4* sum;              // running sums (tile layout) or null
     void* out;                // rgba32F / rgba16F tile or null
-    uint32_t nT, nP, nS;      // triangles, triangle pairs (0: no pair layout), spheres
+    uint32_t nT, nP, nS, nN;  // triangles, triangle pairs (0: no pair layout), spheres, BVH nodes
     float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
     float halfW, halfH;
     int32_t W, H;
@@ -38,7 +40,7 @@ struct KParams {
     uint32_t max_index;       // max Halton index seed+n of this launch (0xFFFFFFFF: unknown/wraps)
 };
 
-size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph);
+size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);
 // Where the workgroup reads the intersection records from.
 enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);

@@ -4,6 +4,8 @@
 
 #include <string.h>
 
+#include <algorithm>
+
 #include "../../include/rtpt.h"
 
 namespace rt {
@@ -238,21 +240,107 @@ static bool same_bits(const float* a, const float* b, int n) {
 // Conservative culling margin: far above the fp32 rounding of the triangle
 // test at the scene's scale (~1e-6 relative), far below the 1e-3 surface
 // offset of raytrace.metal:67.
-static float culling_margin(const rt_float3* verts, uint32_t n_tri) {
+static float culling_margin(const rt_float3* verts, uint32_t n_tri, const SphereGPU* sph = nullptr,
+                            uint32_t n_sph = 0) {
     float ext = 2.5f;
     for (uint32_t k = 0; k < 3 * n_tri; ++k)
         ext = fmaxf(ext, fmaxf(fabsf(verts[k].x), fmaxf(fabsf(verts[k].y), fabsf(verts[k].z))));
+    for (uint32_t k = 0; k < n_sph; ++k)
+        ext = fmaxf(ext, fmaxf(fabsf(sph[k].center.x), fmaxf(fabsf(sph[k].center.y),
+                                                              fabsf(sph[k].center.z))) +
+                             fabsf(sph[k].radius));
     return 4e-5f * ext;
+}
+
+// Depth-first BVH over the spheres (median split of the centroids on the
+// longest axis, <= 4 spheres per leaf).  Only speed depends on its shape: the
+// kernel's traversal skips a node only when no sphere inside can beat the
+// current closest hit, and ties are resolved by sphere id, so the result is
+// that of testing every sphere in id order.
+struct BvhBuild {
+    const SphereGPU* sph;
+    float margin;
+    std::vector<uint32_t> ids;
+    std::vector<BvhNode> nodes;
+
+    void bounds(uint32_t b, uint32_t e, float lo[3], float hi[3], bool centroids) const {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = INFINITY;
+            hi[a] = -INFINITY;
+        }
+        for (uint32_t k = b; k < e; ++k) {
+            const SphereGPU& s = sph[ids[k]];
+            const float c[3] = {s.center.x, s.center.y, s.center.z};
+            const float r = centroids ? 0.0f : fabsf(s.radius);
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = fminf(lo[a], c[a] - r);
+                hi[a] = fmaxf(hi[a], c[a] + r);
+            }
+        }
+    }
+
+    void build(uint32_t b, uint32_t e) {
+        const uint32_t me = (uint32_t)nodes.size();
+        nodes.push_back(BvhNode{});
+        float lo[3], hi[3];
+        bounds(b, e, lo, hi, false);
+        for (int a = 0; a < 3; ++a) {
+            nodes[me].lo[a] = lo[a] - margin;
+            nodes[me].hi[a] = hi[a] + margin;
+        }
+        if (e - b <= 4) {
+            nodes[me].leaf = ((e - b) << 24) | b;
+        } else {
+            float clo[3], chi[3];
+            bounds(b, e, clo, chi, true);
+            int axis = 0;
+            for (int a = 1; a < 3; ++a)
+                if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+            const uint32_t mid = b + (e - b) / 2;
+            std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
+                             [&](uint32_t x, uint32_t y) {
+                                 const float cx[3] = {sph[x].center.x, sph[x].center.y, sph[x].center.z};
+                                 const float cy[3] = {sph[y].center.x, sph[y].center.y, sph[y].center.z};
+                                 return cx[axis] < cy[axis] || (cx[axis] == cy[axis] && x < y);
+                             });
+            nodes[me].leaf = 0;
+            build(b, mid);
+            build(mid, e);
+        }
+        nodes[me].escape = (uint32_t)nodes.size();
+    }
+};
+
+static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint32_t n,
+                             float margin) {
+    out->sph_isect.clear();
+    out->sph_perm.clear();
+    out->sph_nodes.clear();
+    if (n == 0) return;
+    BvhBuild bb;
+    bb.sph = spheres;
+    bb.margin = margin;
+    bb.ids.resize(n);
+    for (uint32_t k = 0; k < n; ++k) bb.ids[k] = k;
+    bb.build(0, n);
+    out->sph_nodes.swap(bb.nodes);
+    out->sph_perm = bb.ids;
+    out->sph_isect.resize(n);
+    for (uint32_t k = 0; k < n; ++k) {
+        const SphereGPU& sp = spheres[bb.ids[k]];
+        const float r2 = sp.radius * sp.radius;
+        const float q[4] = {sp.center.x, sp.center.y, sp.center.z, r2};
+        memcpy(out->sph_isect[k].q, q, sizeof(q));
+    }
 }
 
 // Pair layout: triangles (2k, 2k+1) with the same v0 and one common edge
 // vector S (bitwise, as computed above).  All-or-nothing, so the kernel keeps
 // testing primitives in id order.
-static void build_pairs(CompiledScene* out, const rt_float3* verts) {
+static void build_pairs(CompiledScene* out, const rt_float3* verts, float margin) {
     out->pair_isect.clear();
     const size_t n = out->tri_isect.size();
     if (n == 0 || (n & 1)) return;
-    const float margin = culling_margin(verts, (uint32_t)n);
     std::vector<PairIsect> pairs(n / 2);
     for (size_t k = 0; k < n / 2; ++k) {
         const float* A = out->tri_isect[2 * k].q;      // v0 0..2, e1 3..5, e2 6..8, n 9..11
@@ -360,18 +448,20 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                              em.x, em.y, em.z, mats[k].diffuse.z};
         memcpy(out->tri_shade[k].s, s, sizeof(s));
     }
-    build_pairs(out, verts);
-    out->sph_isect.resize(n_sph);
+    // one margin for every culling box: scene and camera scale
+    const float margin = fmaxf(culling_margin(verts, n_tri, spheres, n_sph),
+                               4e-5f * fmaxf(fabsf(cam.position.x),
+                                             fmaxf(fabsf(cam.position.y), fabsf(cam.position.z))));
+    build_pairs(out, verts, margin);
     out->sph_shade.resize(n_sph);
+    build_sphere_bvh(out, spheres, n_sph, margin);
     for (uint32_t k = 0; k < n_sph; ++k) {
         const SphereGPU& sp = spheres[k];
-        const float r2 = sp.radius * sp.radius;
-        const float q[4] = {sp.center.x, sp.center.y, sp.center.z, r2};
-        memcpy(out->sph_isect[k].q, q, sizeof(q));
         const f3 em = from_abi(sp.material.emissive);
         const float light_flag = (length(em) > 0.0f) ? 1.0f : 0.0f;
-        const float s[8] = {sp.material.diffuse.x, sp.material.diffuse.y, sp.material.diffuse.z,
-                            light_flag, em.x, em.y, em.z, 0.0f};
+        const float s[12] = {sp.material.diffuse.x, sp.material.diffuse.y, sp.material.diffuse.z,
+                             light_flag, em.x, em.y, em.z, 0.0f,
+                             sp.center.x, sp.center.y, sp.center.z, sp.radius * sp.radius};
         memcpy(out->sph_shade[k].s, s, sizeof(s));
     }
     return true;

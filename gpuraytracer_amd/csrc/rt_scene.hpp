@@ -41,9 +41,21 @@ struct TriShade {
 struct SphIsect {
     float q[4];
 };
-// Sphere shading record, 32 B: (diffuse.rgb, light), (emissive.rgb, 0)
+// Sphere BVH node, 2 x float4 = 32 B, nodes in depth-first order (stackless
+// traversal): n0 = (lo.xyz, escape), n1 = (hi.xyz, leaf); escape = index of
+// the node after this subtree; leaf = count << 24 | first (count 0: internal
+// node whose first child is the next node).  Boxes are padded by the culling
+// margin.
+struct BvhNode {
+    float lo[3];
+    uint32_t escape;
+    float hi[3];
+    uint32_t leaf;
+};
+// Sphere shading record by sphere id, 48 B: (diffuse.rgb, light),
+// (emissive.rgb, 0), (c.xyz, r*r)
 struct SphShade {
-    float s[8];
+    float s[12];
 };
 
 // Camera constants of generateCameraRay (sampling.metal:125-157), computed
@@ -64,8 +76,10 @@ struct CompiledScene {
     std::vector<TriIsect> tri_isect;
     std::vector<TriShade> tri_shade;
     std::vector<PairIsect> pair_isect;  // empty unless every (2k, 2k+1) shares v0 + an edge
-    std::vector<SphIsect> sph_isect;
-    std::vector<SphShade> sph_shade;
+    std::vector<SphIsect> sph_isect;    // in BVH leaf order
+    std::vector<uint32_t> sph_perm;     // leaf-order index -> sphere id (shading, ties)
+    std::vector<BvhNode> sph_nodes;
+    std::vector<SphShade> sph_shade;    // by sphere id
 };
 
 // Validates and precomputes; returns false with *err set on bad input.

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RTPT_ABI_VERSION 1
+#define RTPT_ABI_VERSION 2
 
 /* Maximum bounce count: Halton dimensions 2+5b..5+5b must stay inside the
  * 24-entry `primes[]` table (`RTrace/sampling.metal:97-104`); b <= 3. */
@@ -154,6 +154,7 @@ typedef struct rt_scene_info {
     uint32_t n_triangle_pairs;   /* >0: every (2k,2k+1) shares v0 and an edge -> pair records */
     uint32_t n_spheres;
     uint32_t lds_bytes;          /* intersection records staged per workgroup (0: read from global) */
+    uint32_t n_sphere_nodes;     /* sphere BVH nodes (32 B each, staged with the records) */
 } rt_scene_info;
 int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
 

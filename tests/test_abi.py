@@ -77,8 +77,14 @@ def test_seed_helper_range():
 def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.cornell_box(64, 48).describe()
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
-                    "lds_bytes": 18 * 112}
+                    "lds_bytes": 18 * 112, "n_sphere_nodes": 0}
+
+    def bvh_nodes(n):  # median split, <= 4 spheres per leaf (rt_scene.cpp BvhBuild)
+        return 1 if n <= 4 else 1 + bvh_nodes(n // 2) + bvh_nodes(n - n // 2)
+
     info = g.Scene.random_spheres(64, 48, 1000).describe()
-    assert info["n_triangle_pairs"] == 6 and info["lds_bytes"] == 6 * 112 + 1000 * 16
+    assert info["n_sphere_nodes"] == bvh_nodes(1000)
+    assert info["n_triangle_pairs"] == 6
+    assert info["lds_bytes"] == 6 * 112 + bvh_nodes(1000) * 32 + 1000 * 16
     big = g.Scene.random_spheres(16, 8, 5000).describe()
     assert big["lds_bytes"] == 0  # > 64 KiB: records read from global memory
