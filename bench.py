@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -62,7 +63,7 @@ def load_profile_json(name):
     return None
 
 
-def cpu_baseline(scene, width, height, bounces, threads):
+def cpu_baseline(scene, width, height, bounces, threads, cpu_seconds=10.0):
     """Scalar C oracle (the identical shader math) on the host cores."""
     L = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     L.pto_render.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_void_p, ctypes.c_uint32,
@@ -85,15 +86,30 @@ def cpu_baseline(scene, width, height, bounces, threads):
         assert r == 0
         return rows * width * spp / dt / 1e6, rows * width * spp, dt
 
-    heavy = scene.n_spheres > 0
-    v_all, n_all, t_all = run(1 if heavy else 4, 4 if heavy else 1, threads)
-    v_one, n_one, t_one = run(1, 64 if heavy else 8, 1)
+    def sized(seconds, nthreads):
+        # probe on ever denser row sets until one takes >= 0.3 s, then size the
+        # sample to ~`seconds` of CPU work
+        step = 256
+        while True:
+            rate, _, t = run(1, step, nthreads)
+            if t >= 0.3 or step == 1:
+                break
+            step = max(1, step // 4)
+        want = rate * 1e6 * seconds
+        frame = width * height
+        if want >= frame:
+            spp, step = max(1, int(round(want / frame))), 1
+        else:
+            spp, step = 1, max(1, int(math.ceil(frame / want)))
+        v, n, t = run(spp, step, nthreads)
+        rows = "the full" if step == 1 else f"1 in {step} rows of the"
+        return v, f"{rows} {width}x{height} frame at {spp} spp, {bounces} bounces = {n} samples in {t:.2f} s"
+
+    v_all, s_all = sized(cpu_seconds, threads)
+    v_one, s_one = sized(cpu_seconds / 4, 1)
     return {"value": round(v_all, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": (f"{'every 4th row of ' if heavy else ''}the full {width}x{height} frame at "
-                       f"{1 if heavy else 4} spp, {bounces} bounces = {n_all} samples in "
-                       f"{t_all:.2f} s on {threads} threads (scalar C oracle, -O2)"),
-            "single_thread_value": round(v_one, 4),
-            "single_thread_sample": f"{n_one} samples (every {64 if heavy else 8}th row) in {t_one:.2f} s"}
+            "sample": f"{s_all} on {threads} threads (scalar C oracle, -O2)",
+            "single_thread_value": round(v_one, 4), "single_thread_sample": s_one}
 
 
 def main():
@@ -197,7 +213,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: reference Cornell scene (scene.swift), splitmix64 seeds",
+            "data": ("synthetic: reference Cornell scene (scene.swift), splitmix64 seeds"
+                     if args.scene == "cornell" else
+                     f"synthetic: {args.spheres} PCG32 spheres (seed 42) in the Cornell room, "
+                     "splitmix64 seeds"),
             "config": {"workload": workload, "width": W, "height": H, "spp_per_gpu": args.spp,
                        "spp_frame": spp, "bounces": args.bounces,
                        "parallelism": (f"{world} row-interleaved tiles + 1 RCCL gather" if world > 1

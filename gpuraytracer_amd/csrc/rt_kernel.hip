@@ -269,6 +269,104 @@ __device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, con
     return tnear <= tfar;
 }
 
+#ifndef RT_SPH_PACKET
+#define RT_SPH_PACKET 1  // 1: packet walks for camera and bounce-0 shadow rays; 2: + all shadow rays; 3: all
+#endif
+
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Sphere-BVH walks.  The wave walks ONE stackless
+// depth-first path through the escape-index tree: a node is entered when any
+// active lane's ray may hit its padded box.  The node index is therefore wave
+// uniform, node and sphere records are fetched with scalar loads from global
+// memory (no LDS footprint, no bank conflicts) and every lane stays busy; a
+// lane whose own box test failed still tests the leaf's spheres, which cannot
+// change its result because the boxes are conservative.
+template <bool PACKET>
+__device__ __forceinline__ void sphere_closest(const float4* __restrict__ node,
+                                               const float4* __restrict__ sph,
+                                               const uint32_t* __restrict__ perm, uint32_t nN,
+                                               uint32_t nT, f3 o, f3 d, float tmin, float& best,
+                                               int& id) {
+    // Candidates are ranked by (t, sphere id) exactly like the oracle's
+    // id-ordered scan with strict '<', so the visiting order is free.
+    const float a = dot(d, d);
+    const RayBox rb = ray_box(o, d);
+    uint32_t idx = 0;
+    while (idx < nN) {
+        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
+        uint32_t next = PACKET ? wave_uniform(__float_as_uint(n0.w)) : __float_as_uint(n0.w);
+        const bool h = node_hit(n0, n1, rb, tmin, best);
+        if (PACKET ? __builtin_amdgcn_ballot_w64(h) != 0 : h) {
+            const uint32_t leaf = PACKET ? wave_uniform(__float_as_uint(n1.w)) : __float_as_uint(n1.w);
+            if (leaf == 0u) {
+                next = idx + 1;
+            } else {
+                const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                for (uint32_t k = first; k < end; ++k) {
+                    float t;
+                    if (sph_test(sph[k], o, d, a, tmin, 3.0e38f, &t) && t <= best) {
+                        const int sid = (int)(nT + perm[k]);
+                        if (t < best || sid < id) {
+                            best = t;
+                            id = sid;
+                        }
+                    }
+                }
+            }
+        }
+        idx = next;
+    }
+}
+
+template <bool PACKET>
+__device__ __forceinline__ bool sphere_any(const float4* __restrict__ node,
+                                           const float4* __restrict__ sph, uint32_t nN, f3 o,
+                                           f3 d, float tmin, float tmax) {
+    const float a = dot(d, d);
+    const RayBox rb = ray_box(o, d);
+    bool found = false;
+    uint32_t idx = 0;
+    while (idx < nN) {
+        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
+        if (PACKET) {
+            uint32_t next = wave_uniform(__float_as_uint(n0.w));
+            if (__builtin_amdgcn_ballot_w64(!found && node_hit(n0, n1, rb, tmin, tmax)) != 0) {
+                const uint32_t leaf = wave_uniform(__float_as_uint(n1.w));
+                if (leaf == 0u) {
+                    next = idx + 1;
+                } else {
+                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                    for (uint32_t k = first; k < end; ++k) {
+                        float t;
+                        found = found || sph_test(sph[k], o, d, a, tmin, tmax, &t);
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
+                }
+            }
+            idx = next;
+        } else {
+            uint32_t next = __float_as_uint(n0.w);
+            if (node_hit(n0, n1, rb, tmin, tmax)) {
+                const uint32_t leaf = __float_as_uint(n1.w);
+                if (leaf == 0u) {
+                    next = idx + 1;
+                } else {
+                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                    for (uint32_t k = first; k < end; ++k) {
+                        float t;
+                        if (sph_test(sph[k], o, d, a, tmin, tmax, &t)) return true;
+                    }
+                }
+            }
+            idx = next;
+        }
+    }
+    return found;
+}
+
 // closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
 // Primitives are tested in id order; a strictly smaller t wins (ties keep the
 // lower id), exactly as the oracle.
@@ -336,38 +434,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
             }
         }
     }
-    if (SPH) {
-        // Stackless depth-first walk of the sphere BVH (escape indices).  A
-        // node is skipped only if its padded box has no point on the ray in
-        // (tmin, best]; candidates are ranked by (t, sphere id) exactly like
-        // the oracle's id-ordered scan with strict '<'.
-        const float a = dot(d, d);
-        const RayBox rb = ray_box(o, d);
-        uint32_t idx = 0;
-        while (idx < sv.nN) {
-            const float4 n0 = sv.node[2 * idx], n1 = sv.node[2 * idx + 1];
-            uint32_t next = __float_as_uint(n0.w);
-            if (node_hit(n0, n1, rb, tmin, best)) {
-                const uint32_t leaf = __float_as_uint(n1.w);
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        if (sph_test(sv.sph[k], o, d, a, tmin, 3.0e38f, &t) && t <= best) {
-                            const int sid = (int)(sv.nT + sv.sph_perm[k]);
-                            if (t < best || sid < id) {
-                                best = t;
-                                id = sid;
-                            }
-                        }
-                    }
-                }
-            }
-            idx = next;
-        }
-    }
+    if (SPH) sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
     *t_io = best;
     return id;
 }
@@ -377,7 +444,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
 // seg_lo/seg_hi bound every point the ray can accept (t in (tmin, tmax)); a
 // pair whose padded AABB no lane's segment box touches cannot be hit by any
 // lane of the wave and is skipped as a whole.
-template <int GEO, bool SPH>
+template <int GEO, bool SPH, bool PACKET>
 __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
                                         f3 seg_lo, f3 seg_hi) {
     if (GEO == kGeoPairLds) {
@@ -413,28 +480,7 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
                 return true;
         }
     }
-    if (SPH) {
-        const float a = dot(d, d);
-        const RayBox rb = ray_box(o, d);
-        uint32_t idx = 0;
-        while (idx < sv.nN) {
-            const float4 n0 = sv.node[2 * idx], n1 = sv.node[2 * idx + 1];
-            uint32_t next = __float_as_uint(n0.w);
-            if (node_hit(n0, n1, rb, tmin, tmax)) {
-                const uint32_t leaf = __float_as_uint(n1.w);
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        if (sph_test(sv.sph[k], o, d, a, tmin, tmax, &t)) return true;
-                    }
-                }
-            }
-            idx = next;
-        }
-    }
+    if (SPH) return sphere_any<PACKET>(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
     return false;
 }
 
@@ -494,7 +540,7 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     s.thr = s.thr * diffuse;                               // :76
     const f3 seg_lo{fminf(p.x, q.x), fminf(p.y, q.y), fminf(p.z, q.z)};
     const f3 seg_hi{fmaxf(p.x, q.x), fmaxf(p.y, q.y), fmaxf(p.z, q.z)};
-    if (!any_hit<GEO, SPH>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
+    if (!any_hit<GEO, SPH, (b == 0 && RT_SPH_PACKET) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + lc * s.thr;                        // :87-89
     if (b + 1 < B) {                                       // last direction never traced
         const float cu = halton_dim<4 + 5 * b, SMALL>(s.i);           // :93-94
@@ -656,8 +702,11 @@ size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 #ifndef RT_MIN_WAVES_PER_EU
 #define RT_MIN_WAVES_PER_EU 8  // 8 waves/SIMD (<= 64 VGPRs): +4.5% measured over 7
 #endif
+#ifndef RT_MIN_WAVES_PER_EU_SPH
+#define RT_MIN_WAVES_PER_EU_SPH 8
+#endif
 template <int B, int GEO, bool SPH, bool SMALL>
-__global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace_kernel(KParams P) {
+__global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_MIN_WAVES_PER_EU) void path_trace_kernel(KParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
     sv.nT = P.nT;
@@ -668,24 +717,15 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
         const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
-        if (SPH) {
-            const uint32_t nn4 = 2u * P.nN;
-            for (uint32_t k = threadIdx.x; k < nn4; k += kBlockThreads)
-                lds[ng4 + k] = P.sph_nodes[k];
-            for (uint32_t k = threadIdx.x; k < sv.nS; k += kBlockThreads)
-                lds[ng4 + nn4 + k] = P.sph_isect[k];
-        }
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
-        sv.node = lds + ng4;
-        sv.sph = lds + ng4 + 2u * P.nN;
     } else {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
-        sv.node = P.sph_nodes;
-        sv.sph = P.sph_isect;
     }
+    sv.node = P.sph_nodes;  // sphere BVH: scalar loads from global memory
+    sv.sph = P.sph_isect;
     sv.nN = SPH ? P.nN : 0u;
     sv.sph_perm = P.sph_perm;
 
@@ -748,15 +788,10 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
     float4* scene = lds + kSortF4;  // sort buffers first: compile-time offsets
     for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) scene[k] = P.pair_isect[k];
     sv.nN = SPH ? P.nN : 0u;
-    if (SPH) {
-        for (uint32_t k = threadIdx.x; k < 2u * sv.nN; k += kBlockThreads) scene[ng4 + k] = P.sph_nodes[k];
-        for (uint32_t k = threadIdx.x; k < sv.nS; k += kBlockThreads)
-            scene[ng4 + 2u * sv.nN + k] = P.sph_isect[k];
-    }
     sv.tri = scene;
     sv.pair = scene;
-    sv.node = scene + ng4;
-    sv.sph = scene + ng4 + 2u * sv.nN;
+    sv.node = P.sph_nodes;
+    sv.sph = P.sph_isect;
     sv.sph_perm = P.sph_perm;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -876,8 +911,10 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
 }  // namespace
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes) {
+    (void)n_sph;  // sphere BVH nodes and records stay in global memory (scalar loads)
+    (void)n_nodes;
     const uint32_t geo4 = n_pairs ? kPairF4 * n_pairs : 3u * n_tri;
-    return (size_t)(geo4 + 2u * n_nodes + n_sph) * sizeof(float4);
+    return (size_t)geo4 * sizeof(float4);
 }
 
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,

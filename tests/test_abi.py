@@ -85,6 +85,7 @@ def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.random_spheres(64, 48, 1000).describe()
     assert info["n_sphere_nodes"] == bvh_nodes(1000)
     assert info["n_triangle_pairs"] == 6
-    assert info["lds_bytes"] == 6 * 112 + bvh_nodes(1000) * 32 + 1000 * 16
+    # only the triangle pairs are staged; the sphere BVH is read with scalar loads
+    assert info["lds_bytes"] == 6 * 112
     big = g.Scene.random_spheres(16, 8, 5000).describe()
-    assert big["lds_bytes"] == 0  # > 64 KiB: records read from global memory
+    assert big["lds_bytes"] == 6 * 112 and big["n_sphere_nodes"] == bvh_nodes(5000)

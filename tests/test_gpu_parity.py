@@ -80,8 +80,8 @@ def test_spheres_1000_vs_oracle():
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), "spheres1000")
 
 
-def test_large_sphere_scene_uses_global_path():
-    # > 64 KiB of intersection records: the kernel reads from global, not LDS
+def test_large_sphere_scene_bvh():
+    # 5000 spheres: deep BVH (2047 nodes), ties and leaves far beyond the 1000-sphere case
     s = Scene.random_spheres(24, 16, 5000, seed=9)
     sd = seed_splitmix(24, 16)
     with Renderer(s, seeds=sd) as r:
