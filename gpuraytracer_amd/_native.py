@@ -96,6 +96,11 @@ RT_MAX_BOUNCES = 4
 STATUS = {0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_NO_DEVICE", 3: "RT_ERR_OUT_OF_MEMORY",
           4: "RT_ERR_LAUNCH", 5: "RT_ERR_STATE", 6: "RT_ERR_COMM"}
 
+class MisParamsC(ctypes.Structure):  # rt_mis_params
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                ("camera_rays", "mis_samples", "row_start", "row_step", "row_count", "flags")]
+
+
 # Every entry point of include/rtpt.h: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 SIGNATURES = {
@@ -124,6 +129,13 @@ SIGNATURES = {
                                                ctypes.POINTER(SquareLightGPU),
                                                ctypes.POINTER(ctypes.c_uint32),
                                                ctypes.POINTER(SphereGPU)]),
+    "rt_render_mis": (ctypes.c_int, [_P, ctypes.POINTER(MisParamsC), _P, _P]),
+    "rt_scene_cornell_box_mis": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32,
+                                                ctypes.POINTER(CameraGPU),
+                                                ctypes.POINTER(MaterialGPU),
+                                                ctypes.POINTER(float3),
+                                                ctypes.POINTER(SquareLightGPU),
+                                                ctypes.POINTER(ctypes.c_uint32)]),
     "rt_tonemap_rgba8": (None, [_P, ctypes.c_size_t, _P]),
     "rt_scene_describe": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(SceneInfo)]),
 }

@@ -14,6 +14,7 @@
 
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/rtpt.h"
 #include "rt_kernel.hpp"
@@ -30,6 +31,11 @@ struct rt_ctx {
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
     uint32_t* d_sph_perm = nullptr;
+    float4* d_mis_shade = nullptr;
+    float4* d_mis_tab = nullptr;   // Halton table of the MIS integrator
+    uint32_t mis_tab_S = 0;        // samples per strategy it was built for
+    void* d_out8 = nullptr;        // staging for host RGBA8 outputs
+    size_t out8_cap = 0;
     uint32_t* d_seeds = nullptr;
     bool seeds_ready = false;
     uint32_t seed_max = 0xFFFFFFFFu;  // max seed value (bounds the Halton index)
@@ -95,6 +101,9 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_sph_nodes);
     (void)hipFree(c->d_sph_perm);
+    (void)hipFree(c->d_mis_shade);
+    (void)hipFree(c->d_mis_tab);
+    (void)hipFree(c->d_out8);
     (void)hipFree(c->d_seeds);
     (void)hipFree(c->d_sum);
     (void)hipFree(c->d_out);
@@ -236,6 +245,149 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     return RT_OK;
 }
 
+// halton(i, d) of the SwiftPM kernel (Sources/gpuRaytracer/shaders.metal:32-47),
+// the same loop as RTrace/sampling.metal:107-122.
+float halton_host(uint32_t i, uint32_t d) {
+    static const uint32_t primes[24] = RT_PRIMES_INIT;
+    const uint32_t b = primes[d];
+    float f = 1.0f;
+    const float invB = 1.0f / (float)b;
+    float r = 0.0f;
+    while (i > 0) {
+        f = f * invB;
+        r = r + f * (float)(i % b);
+        i = i / b;
+    }
+    return r;
+}
+
+// MIS sample table: the u of every strategy depends only on the sample index
+// (haltonRandom(i, d), shaders.metal:556,564,584,595,617), not on the pixel.
+int mis_table(rt_ctx* c, uint32_t S) {
+    if (c->d_mis_tab && c->mis_tab_S == S) return RT_OK;
+    std::vector<float> t((size_t)S * 12u);
+    for (uint32_t i = 0; i < S; ++i) {
+        float* q = &t[(size_t)i * 12u];
+        q[0] = halton_host(i, 0);            // light sampling :556
+        q[1] = halton_host(i, 1);
+        q[2] = 0.0f;
+        q[3] = 0.0f;
+        q[4] = halton_host(i + S, 2);        // cosine :564
+        q[5] = halton_host(i + S, 3);
+        q[6] = halton_host(i, 6);            // its secondary NEE :584
+        q[7] = halton_host(i, 7);
+        q[8] = halton_host(i + 2 * S, 4);    // VNDF :595
+        q[9] = halton_host(i + 2 * S, 5);
+        q[10] = halton_host(i + S, 6);       // its secondary NEE :617
+        q[11] = halton_host(i + S, 7);
+    }
+    (void)hipFree(c->d_mis_tab);
+    c->d_mis_tab = nullptr;
+    c->mis_tab_S = 0;
+    hipError_t e = upload(&c->d_mis_tab, t.data(), t.size() * sizeof(float), c->stream);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_OUT_OF_MEMORY, "MIS table upload", e);
+    c->mis_tab_S = S;
+    return RT_OK;
+}
+
+int ensure_staging(rt_ctx* c, void** buf, size_t* cap, size_t bytes, const char* what) {
+    if (*cap >= bytes) return RT_OK;
+    (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(buf, bytes);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_OUT_OF_MEMORY, what, e);
+    *cap = bytes;
+    return RT_OK;
+}
+
+int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8) {
+    if (!p) return fail(c, RT_ERR_INVALID_ARG, "params is null");
+    if (!out && !out8) return fail(c, RT_ERR_INVALID_ARG, "both outputs are null");
+    if (!c->scene.sph_isect.empty())
+        return fail(c, RT_ERR_INVALID_ARG,
+                    "the MIS integrator traces triangle scenes only (shaders.metal:459-509)");
+    if (c->scene.tri_isect.empty()) return fail(c, RT_ERR_INVALID_ARG, "scene has no triangles");
+    if (p->camera_rays == 0) return fail(c, RT_ERR_INVALID_ARG, "camera_rays must be >= 1");
+    if (p->mis_samples < 3 || p->mis_samples / 3u > (1u << 20))
+        return fail(c, RT_ERR_INVALID_ARG, "mis_samples must be in [3, 3 * 2^20]");
+    rt_render_params rp;
+    memset(&rp, 0, sizeof(rp));
+    rp.row_start = p->row_start;
+    rp.row_step = p->row_step;
+    rp.row_count = p->row_count;
+    uint32_t start, step, count;
+    if (!resolve_rows(c, &rp, &start, &step, &count))
+        return fail(c, RT_ERR_INVALID_ARG, "row partition outside the frame");
+    const uint32_t S = p->mis_samples / 3u;  // samplesPerStrategy (:546)
+    int st = mis_table(c, S);
+    if (st != RT_OK) return st;
+    const bool dev = (p->flags & RT_OUT_DEVICE) != 0;
+    const size_t pixels = (size_t)count * (size_t)c->scene.cam.W;
+    float4* kout = nullptr;
+    uchar4* kout8 = nullptr;
+    if (out) {
+        if (!dev && (st = ensure_staging(c, &c->d_out, &c->out_cap, pixels * 16u, "hipMalloc(out staging)")) != RT_OK)
+            return st;
+        kout = dev ? reinterpret_cast<float4*>(out) : reinterpret_cast<float4*>(c->d_out);
+    }
+    if (out8) {
+        if (!dev && (st = ensure_staging(c, &c->d_out8, &c->out8_cap, pixels * 4u, "hipMalloc(out8 staging)")) != RT_OK)
+            return st;
+        kout8 = dev ? reinterpret_cast<uchar4*>(out8) : reinterpret_cast<uchar4*>(c->d_out8);
+    }
+
+    rt::MisParams K;
+    memset(&K, 0, sizeof(K));
+    K.tri_isect = c->d_tri_isect;
+    K.pair_isect = c->d_pair_isect;
+    K.mis_shade = c->d_mis_shade;
+    K.u_tab = c->d_mis_tab;
+    K.out = kout;
+    K.out8 = kout8;
+    K.nT = (uint32_t)c->scene.tri_isect.size();
+    K.nP = (uint32_t)c->scene.pair_isect.size();
+    const rt::CamConst& cam = c->scene.cam;
+    memcpy(K.cam_pos, cam.pos, sizeof(K.cam_pos));
+    memcpy(K.cam_u, cam.u, sizeof(K.cam_u));
+    memcpy(K.cam_v, cam.v, sizeof(K.cam_v));
+    memcpy(K.cam_w, cam.w, sizeof(K.cam_w));
+    K.halfW = cam.halfW;
+    K.halfH = cam.halfH;
+    K.W = cam.W;
+    K.H = cam.H;
+    const rt::MisLightConst& ml = c->scene.mis_light;
+    memcpy(K.l_center, ml.center, sizeof(K.l_center));
+    memcpy(K.l_tangent, ml.tangent, sizeof(K.l_tangent));
+    memcpy(K.l_bitangent, ml.bitangent, sizeof(K.l_bitangent));
+    memcpy(K.l_radiance, ml.radiance, sizeof(K.l_radiance));
+    K.l_width = ml.width;
+    K.l_depth = ml.depth;
+    K.l_area = ml.area;
+    K.exposure = ml.exposure;
+    K.camera_rays = p->camera_rays;
+    K.S = S;
+    K.row_start = start;
+    K.row_step = step;
+    K.row_count = count;
+
+    hipError_t e;
+    (void)hipEventRecord(c->ev0, c->stream);
+    e = rt::launch_mis(K, c->scene_mem, c->stream);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "mis launch", e);
+    (void)hipEventRecord(c->ev1, c->stream);
+    c->timed = true;
+    if (out && !dev &&
+        (e = hipMemcpyAsync(out, kout, pixels * 16u, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpyAsync(out)", e);
+    if (out8 && !dev &&
+        (e = hipMemcpyAsync(out8, kout8, pixels * 4u, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpyAsync(out8)", e);
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(c, RT_ERR_LAUNCH, "mis execution", e);
+    return RT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -305,7 +457,8 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_nodes, s.sph_nodes.data(), s.sph_nodes.size() * sizeof(rt::BvhNode), c->stream)) != hipSuccess ||
-            (e = upload(&c->d_sph_perm, s.sph_perm.data(), s.sph_perm.size() * sizeof(uint32_t), c->stream)) != hipSuccess) {
+            (e = upload(&c->d_sph_perm, s.sph_perm.data(), s.sph_perm.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_mis_shade, s.mis_shade.data(), s.mis_shade.size() * sizeof(rt::MisShade), c->stream)) != hipSuccess) {
             status = RT_ERR_OUT_OF_MEMORY; msg = std::string("scene upload: ") + hipGetErrorString(e); break;
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
@@ -428,6 +581,22 @@ int rt_scene_cornell_box(int32_t width, int32_t height, CameraGPU* camera, Mater
     if (!camera || !materials || !vertices || !light || !n_triangles || width <= 0 || height <= 0)
         return RT_ERR_INVALID_ARG;
     const rt::Scene s = rt::init_cornell_box(width, height);
+    fill_scene_arrays(s, camera, materials, vertices, light);
+    *n_triangles = (uint32_t)s.triangles.size();
+    return RT_OK;
+}
+
+int rt_render_mis(rt_ctx* ctx, const rt_mis_params* params, float* out_rgba32f, uint8_t* out_rgba8) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    DeviceGuard g(ctx->device);
+    return render_mis_impl(ctx, params, out_rgba32f, out_rgba8);
+}
+
+int rt_scene_cornell_box_mis(int32_t width, int32_t height, CameraGPU* camera, MaterialGPU* materials,
+                             rt_float3* vertices, SquareLightGPU* light, uint32_t* n_triangles) {
+    if (!camera || !materials || !vertices || !light || !n_triangles || width <= 0 || height <= 0)
+        return RT_ERR_INVALID_ARG;
+    const rt::Scene s = rt::init_cornell_box_mis(width, height);
     fill_scene_arrays(s, camera, materials, vertices, light);
     *n_triangles = (uint32_t)s.triangles.size();
     return RT_OK;

@@ -17,6 +17,7 @@
 #include <hip/hip_fp16.h>
 
 #include "rt_kernel.hpp"
+#include "rt_trace.hpp"
 
 namespace rt {
 
@@ -103,385 +104,6 @@ template <uint32_t D, bool SMALL>
 __device__ __forceinline__ float halton_dim(uint32_t i) {
     if (SMALL) return halton_small<D>(i);
     return halton<D>(i);
-}
-
-__device__ __forceinline__ f3 ld_f3(const float* p) { return f3{p[0], p[1], p[2]}; }
-
-// Ray/triangle test of DESIGN.md §3.5 (stands in for Metal's intersector).
-// The oracle negates (bu, bv, tn, den) when den < 0; here the same exact
-// negation is an XOR with den's sign bit, |den| folds into the compare, and tn
-// (with the IEEE division) is only formed for lanes inside the triangle.
-__device__ __forceinline__ bool tri_test(const float4& A, const float4& Bq, const float4& C, f3 o,
-                                         f3 d, float tmin, float tmax, float* t_out) {
-    const f3 v0{A.x, A.y, A.z}, e1{A.w, Bq.x, Bq.y}, e2{Bq.z, Bq.w, C.x}, n{C.y, C.z, C.w};
-    const f3 tv = o - v0;
-    const f3 c = cross(tv, d);
-    const float den = dot(n, d);
-    const uint32_t sgn = __float_as_uint(den) & 0x80000000u;
-    const uint32_t nsgn = sgn ^ 0x80000000u;
-    const float bu = __uint_as_float(__float_as_uint(dot(e2, c)) ^ nsgn);  // -dot(e2,c), sign-normalised
-    const float bv = __uint_as_float(__float_as_uint(dot(e1, c)) ^ sgn);
-    const float aden = fabsf(den);
-    if (aden > 0.0f && bu >= 0.0f && bv >= 0.0f && bu + bv <= aden) {
-        const float tn = __uint_as_float(__float_as_uint(dot(n, tv)) ^ nsgn);  // -dot(n,tv)
-        const float t = tn / aden;
-        if (t > tmin && t < tmax) {
-            *t_out = t;
-            return true;
-        }
-    }
-    return false;
-}
-
-// Two consecutive triangles A=(v0,..), B=(v0,..) that share v0 and one edge S
-// (every quad of the reference scene, scene.swift:81-138, :212-240).  The
-// per-triangle test above is evaluated for A then B with the common terms
-// tv = o - v0, c = cross(tv, d) and dot(S, c) computed once: bit-identical to
-// two tri_test calls, ~25% fewer VALU operations.  Record (5 x float4):
-//   r0 = (v0.xyz, S.x)  r1 = (S.yz, eA.xy)  r2 = (eA.z, nA.xyz)
-//   r3 = (eB.xyz, nB.x) r4 = (nB.yz, m, 0)
-// m = 0 when A.e1 == S == B.e2, 0x80000000 when A.e2 == S == B.e1; eA / eB
-// are the other edges.  bu+bv and the bu,bv >= 0 tests are symmetric in
-// (bu, bv), so only the signs of the two terms matter.
-struct PairDots {
-    float denA, denB;  // dot(n, d)
-    uint32_t a1, a2, b1, b2;  // sign-normalised barycentric terms (bits)
-    f3 tv;
-};
-
-__device__ __forceinline__ PairDots pair_dots(const float4& r0, const float4& r1,
-                                              const float4& r2, const float4& r3,
-                                              const float4& r4, f3 o, f3 d) {
-    PairDots q;
-    const f3 v0{r0.x, r0.y, r0.z}, S{r0.w, r1.x, r1.y}, eA{r1.z, r1.w, r2.x};
-    const f3 nA{r2.y, r2.z, r2.w}, eB{r3.x, r3.y, r3.z}, nB{r3.w, r4.x, r4.y};
-    const uint32_t m = __float_as_uint(r4.z);
-    q.tv = o - v0;
-    const f3 c = cross(q.tv, d);
-    const uint32_t s = __float_as_uint(dot(S, c));
-    const uint32_t ea = __float_as_uint(dot(eA, c));
-    const uint32_t eb = __float_as_uint(dot(eB, c));
-    q.denA = dot(nA, d);
-    q.denB = dot(nB, d);
-    const uint32_t sA = (__float_as_uint(q.denA) & 0x80000000u) ^ m;
-    const uint32_t sB = (__float_as_uint(q.denB) & 0x80000000u) ^ m;
-    q.a1 = s ^ sA;
-    q.a2 = ea ^ sA ^ 0x80000000u;
-    q.b1 = s ^ sB ^ 0x80000000u;
-    q.b2 = eb ^ sB;
-    return q;
-}
-
-__device__ __forceinline__ bool bary_ok(float den, uint32_t t1, uint32_t t2) {
-    const float u = __uint_as_float(t1), v = __uint_as_float(t2);
-    return fabsf(den) > 0.0f && u >= 0.0f && v >= 0.0f && u + v <= fabsf(den);
-}
-
-// t of a triangle whose barycentric test passed: -dot(n, tv) / den, sign-normalised
-__device__ __forceinline__ float pair_t(f3 n, f3 tv, float den) {
-    const uint32_t nsgn = (__float_as_uint(den) & 0x80000000u) ^ 0x80000000u;
-    const float tn = __uint_as_float(__float_as_uint(dot(n, tv)) ^ nsgn);
-#ifdef RT_TIMING_APPROX_DIV  // timing-only experiment, NOT bit-exact
-    return tn * __builtin_amdgcn_rcpf(fabsf(den));
-#else
-    return tn / fabsf(den);
-#endif
-}
-
-// intersectSphere (shaders_old.metal:108-136) with the DESIGN.md §3.6 root rule.
-__device__ __forceinline__ bool sph_test(const float4& S, f3 o, f3 d, float a, float tmin,
-                                         float tmax, float* t_out) {
-    const f3 oc = o - f3{S.x, S.y, S.z};
-    const float b = 2.0f * dot(oc, d);
-    const float cc = dot(oc, oc) - S.w;
-    const float disc = b * b - (4.0f * a) * cc;
-    if (disc > 0.0f) {
-        const float sq = sqrtf(disc);
-        const float a2 = 2.0f * a;
-        const float t1 = (-b - sq) / a2;
-        const float t2 = (-b + sq) / a2;
-        const float t = (t1 > tmin) ? t1 : t2;
-        if (t > tmin && t < tmax) {
-            *t_out = t;
-            return true;
-        }
-    }
-    return false;
-}
-
-// Diagnostic counters (only in an -DRT_STATS build; read with rt_debug_stats).
-// Slot groups of 4 per query kind q (0: camera closest hit, 1: bounce closest
-// hit, 2: shadow any-hit): [4q] pair records visited per wave, [4q+1] records
-// tested, [4q+2] active lanes summed over tested records, [4q+3] division blocks.
-#ifdef RT_STATS
-__device__ unsigned long long g_rt_stats[16];
-__device__ __forceinline__ void stat_wave(int slot, unsigned long long v) {
-    const unsigned long long m = __ballot(1);
-    if ((threadIdx.x & 63u) == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(&g_rt_stats[slot], v);
-}
-#define RT_STAT(slot, v) stat_wave((slot), (v))
-#else
-#define RT_STAT(slot, v) ((void)0)
-#endif
-
-// Where the intersection records live for one launch.
-enum Geo : int {
-    kGeoTriLds = 0,     // single-triangle records staged in LDS
-    kGeoPairLds = 1,    // shared-edge pair records staged in LDS
-    kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
-};
-
-struct SceneView {
-    const float4* tri;        // 3 float4 per triangle (single layout)
-    const float4* pair;       // kPairF4 float4 per triangle pair (pair layout)
-    const float4* sph;        // 1 float4 per sphere, BVH leaf order
-    const float4* node;       // 2 float4 per sphere-BVH node
-    const uint32_t* sph_perm; // leaf order -> sphere id (global memory)
-    uint32_t nT, nP, nS, nN;
-};
-
-// Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
-// node boxes carry the culling margin, so only speed depends on its rounding.
-struct RayBox {
-    f3 invd, oinv;
-};
-
-__device__ __forceinline__ float safe_rcp(float v) {
-    return __builtin_amdgcn_rcpf(fabsf(v) < 1e-20f ? copysignf(1e-20f, v) : v);
-}
-
-__device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
-    RayBox r;
-    r.invd = f3{safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z)};
-    r.oinv = f3{o.x * r.invd.x, o.y * r.invd.y, o.z * r.invd.z};
-    return r;
-}
-
-// Conservative ray/box overlap on (tmin, tmax): false only if no point of the
-// padded box lies on the ray inside that range.
-__device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, const RayBox& rb,
-                                         float tmin, float tmax) {
-    const float tx0 = fmaf(n0.x, rb.invd.x, -rb.oinv.x), tx1 = fmaf(n1.x, rb.invd.x, -rb.oinv.x);
-    const float ty0 = fmaf(n0.y, rb.invd.y, -rb.oinv.y), ty1 = fmaf(n1.y, rb.invd.y, -rb.oinv.y);
-    const float tz0 = fmaf(n0.z, rb.invd.z, -rb.oinv.z), tz1 = fmaf(n1.z, rb.invd.z, -rb.oinv.z);
-    const float tnear = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tfar = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
-    return tnear <= tfar;
-}
-
-#ifndef RT_SPH_PACKET
-#define RT_SPH_PACKET 1  // 1: packet walks for camera and bounce-0 shadow rays; 2: + all shadow rays; 3: all
-#endif
-
-__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-
-// Sphere-BVH walks.  The wave walks ONE stackless
-// depth-first path through the escape-index tree: a node is entered when any
-// active lane's ray may hit its padded box.  The node index is therefore wave
-// uniform, node and sphere records are fetched with scalar loads from global
-// memory (no LDS footprint, no bank conflicts) and every lane stays busy; a
-// lane whose own box test failed still tests the leaf's spheres, which cannot
-// change its result because the boxes are conservative.
-template <bool PACKET>
-__device__ __forceinline__ void sphere_closest(const float4* __restrict__ node,
-                                               const float4* __restrict__ sph,
-                                               const uint32_t* __restrict__ perm, uint32_t nN,
-                                               uint32_t nT, f3 o, f3 d, float tmin, float& best,
-                                               int& id) {
-    // Candidates are ranked by (t, sphere id) exactly like the oracle's
-    // id-ordered scan with strict '<', so the visiting order is free.
-    const float a = dot(d, d);
-    const RayBox rb = ray_box(o, d);
-    uint32_t idx = 0;
-    while (idx < nN) {
-        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
-        uint32_t next = PACKET ? wave_uniform(__float_as_uint(n0.w)) : __float_as_uint(n0.w);
-        const bool h = node_hit(n0, n1, rb, tmin, best);
-        if (PACKET ? __builtin_amdgcn_ballot_w64(h) != 0 : h) {
-            const uint32_t leaf = PACKET ? wave_uniform(__float_as_uint(n1.w)) : __float_as_uint(n1.w);
-            if (leaf == 0u) {
-                next = idx + 1;
-            } else {
-                const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                for (uint32_t k = first; k < end; ++k) {
-                    float t;
-                    if (sph_test(sph[k], o, d, a, tmin, 3.0e38f, &t) && t <= best) {
-                        const int sid = (int)(nT + perm[k]);
-                        if (t < best || sid < id) {
-                            best = t;
-                            id = sid;
-                        }
-                    }
-                }
-            }
-        }
-        idx = next;
-    }
-}
-
-template <bool PACKET>
-__device__ __forceinline__ bool sphere_any(const float4* __restrict__ node,
-                                           const float4* __restrict__ sph, uint32_t nN, f3 o,
-                                           f3 d, float tmin, float tmax) {
-    const float a = dot(d, d);
-    const RayBox rb = ray_box(o, d);
-    bool found = false;
-    uint32_t idx = 0;
-    while (idx < nN) {
-        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
-        if (PACKET) {
-            uint32_t next = wave_uniform(__float_as_uint(n0.w));
-            if (__builtin_amdgcn_ballot_w64(!found && node_hit(n0, n1, rb, tmin, tmax)) != 0) {
-                const uint32_t leaf = wave_uniform(__float_as_uint(n1.w));
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        found = found || sph_test(sph[k], o, d, a, tmin, tmax, &t);
-                    }
-                    if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
-                }
-            }
-            idx = next;
-        } else {
-            uint32_t next = __float_as_uint(n0.w);
-            if (node_hit(n0, n1, rb, tmin, tmax)) {
-                const uint32_t leaf = __float_as_uint(n1.w);
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        if (sph_test(sph[k], o, d, a, tmin, tmax, &t)) return true;
-                    }
-                }
-            }
-            idx = next;
-        }
-    }
-    return found;
-}
-
-// closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
-// Primitives are tested in id order; a strictly smaller t wins (ties keep the
-// lower id), exactly as the oracle.
-// With CULL (used for coherent camera rays) a pair is skipped when no lane's
-// box around its current candidate segment [o, o + d*best] touches the pair's
-// padded AABB: any hit that could still win has t < best and lies inside it.
-template <int GEO, bool SPH, bool CULL, int QT = 0>
-__device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, float tmin,
-                                           float* t_io) {
-    float best = *t_io;
-    int id = -1;
-    if (GEO == kGeoPairLds) {
-        f3 seg_lo, seg_hi;
-        if (CULL) {
-            const f3 e = o + d * best;
-            seg_lo = f3{fminf(o.x, e.x), fminf(o.y, e.y), fminf(o.z, e.z)};
-            seg_hi = f3{fmaxf(o.x, e.x), fmaxf(o.y, e.y), fmaxf(o.z, e.z)};
-        }
-        for (uint32_t k = 0; k < sv.nP; ++k) {
-            const float4* r = sv.pair + kPairF4 * k;
-            RT_STAT(4 * QT, 1);
-            if (CULL) {
-                const float4 b0 = r[5], b1 = r[6];
-                const bool overlap = seg_lo.x <= b0.w && seg_hi.x >= b0.x && seg_lo.y <= b1.x &&
-                                     seg_hi.y >= b0.y && seg_lo.z <= b1.y && seg_hi.z >= b0.z;
-                if (!__any(overlap)) continue;
-            }
-            RT_STAT(4 * QT + 1, 1);
-            RT_STAT(4 * QT + 2, __popcll(__ballot(1)));
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
-            const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
-            const bool pa = bary_ok(q.denA, q.a1, q.a2);
-            const bool pb = bary_ok(q.denB, q.b1, q.b2);
-            if (pa || pb) {
-                RT_STAT(4 * QT + 3, 1);
-                // One division for whichever of A, B the ray passes (A first);
-                // a ray on the shared edge passes both and also runs B after.
-                const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
-                const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
-                if (t > tmin && t < best) {
-                    best = t;
-                    id = (int)(pa ? 2 * k : 2 * k + 1);
-                }
-                if (pa && pb) {
-                    const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
-                    if (t2 > tmin && t2 < best) {
-                        best = t2;
-                        id = (int)(2 * k + 1);
-                    }
-                }
-                if (CULL) {
-                    const f3 e = o + d * best;
-                    seg_lo = f3{fminf(o.x, e.x), fminf(o.y, e.y), fminf(o.z, e.z)};
-                    seg_hi = f3{fmaxf(o.x, e.x), fmaxf(o.y, e.y), fmaxf(o.z, e.z)};
-                }
-            }
-        }
-    } else {
-        for (uint32_t k = 0; k < sv.nT; ++k) {
-            float t;
-            if (tri_test(sv.tri[3 * k], sv.tri[3 * k + 1], sv.tri[3 * k + 2], o, d, tmin, best,
-                         &t)) {
-                best = t;
-                id = (int)k;
-            }
-        }
-    }
-    if (SPH) sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
-    *t_io = best;
-    return id;
-}
-
-// any hit, accept_any_intersection(true) (raytrace.metal:79-85).  The boolean
-// result does not depend on the order of the tests.
-// seg_lo/seg_hi bound every point the ray can accept (t in (tmin, tmax)); a
-// pair whose padded AABB no lane's segment box touches cannot be hit by any
-// lane of the wave and is skipped as a whole.
-template <int GEO, bool SPH, bool PACKET>
-__device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
-                                        f3 seg_lo, f3 seg_hi) {
-    if (GEO == kGeoPairLds) {
-        for (uint32_t k = 0; k < sv.nP; ++k) {
-            const float4* r = sv.pair + kPairF4 * k;
-            const float4 b0 = r[5], b1 = r[6];
-            const bool overlap = seg_lo.x <= b0.w && seg_hi.x >= b0.x && seg_lo.y <= b1.x &&
-                                 seg_hi.y >= b0.y && seg_lo.z <= b1.y && seg_hi.z >= b0.z;
-            RT_STAT(8, 1);
-            if (!__any(overlap)) continue;
-            RT_STAT(9, 1);
-            RT_STAT(10, __popcll(__ballot(1)));
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
-            const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
-            const bool pa = bary_ok(q.denA, q.a1, q.a2);
-            const bool pb = bary_ok(q.denB, q.b1, q.b2);
-            if (pa || pb) {
-                RT_STAT(11, 1);
-                const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
-                const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
-                if (t > tmin && t < tmax) return true;
-                if (pa && pb) {
-                    const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
-                    if (t2 > tmin && t2 < tmax) return true;
-                }
-            }
-        }
-    } else {
-        for (uint32_t k = 0; k < sv.nT; ++k) {
-            float t;
-            if (tri_test(sv.tri[3 * k], sv.tri[3 * k + 1], sv.tri[3 * k + 2], o, d, tmin, tmax,
-                         &t))
-                return true;
-        }
-    }
-    if (SPH) return sphere_any<PACKET>(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
-    return false;
 }
 
 struct PathState {

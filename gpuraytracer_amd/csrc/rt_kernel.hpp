@@ -45,6 +45,27 @@ size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32
 enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
 hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
+// Arguments of the MIS integrator kernel (rt_mis.hip; Sources/gpuRaytracer/
+// shaders.metal:635-707).
+struct MisParams {
+    const float4* tri_isect;   // 3 float4 per triangle
+    const float4* pair_isect;  // kPairF4 float4 per pair, or null
+    const float4* mis_shade;   // 3 float4 per triangle (MisShade)
+    const float4* u_tab;       // 3 float4 per MIS sample index i < S (Halton table)
+    float4* out;               // (sum over camera rays, camera_rays) per pixel, or null
+    uchar4* out8;              // writeToPixelBuffer RGBA8, or null
+    uint32_t nT, nP;
+    float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
+    float halfW, halfH;
+    int32_t W, H;
+    float l_center[3], l_tangent[3], l_bitangent[3], l_radiance[3];
+    float l_width, l_depth, l_area, exposure;
+    uint32_t camera_rays, S;   // S = misSamples / 3 (samples per strategy)
+    uint32_t row_start, row_step, row_count;
+};
+hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream);
+size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs);
+
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 
 }  // namespace rt

@@ -76,4 +76,79 @@ RT_HD void sincos_pt(float x, float* s_out, float* c_out) {
     *c_out = ((q + 1) & 2) ? -cc : cc;
 }
 
+// ---- MIS integrator helpers (Sources/gpuRaytracer/shaders.metal) ---------
+
+RT_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+RT_HD float u2f(uint32_t x) { return __builtin_bit_cast(float, x); }
+
+// hash (shaders.metal:58-65)
+RT_HD uint32_t mis_hash(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+// randomFloat (:67-69): float(h) / (float(0xffffffff) + 1) = float(h) * 2^-32, exactly
+RT_HD float mis_unit(uint32_t h) { return (float)h * 2.3283064365386963e-10f; }
+
+// buildOrthonormalBasis (:159-172)
+RT_HD void onb(f3 n, f3* t, f3* b) {
+    const f3 a = fabsf(n.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
+    *t = normalize(a - n * dot(a, n));
+    *b = cross(n, *t);
+}
+
+// Portable natural log for normal x > 0 (cephes logf reduction and
+// polynomial, Horner steps as explicit fmaf).
+RT_HD float log_pt(float x) {
+    const uint32_t bx = f2u(x);
+    int e = (int)(bx >> 23) - 126;                     // x = m * 2^e, m in [0.5, 1)
+    float m = u2f((bx & 0x007FFFFFu) | 0x3F000000u);
+    if (m < 0.707106781f) {
+        e -= 1;
+        m = m + m - 1.0f;
+    } else {
+        m = m - 1.0f;
+    }
+    const float z = m * m;
+    float y = 7.0376836292e-2f;
+    y = fmaf(y, m, -1.1514610310e-1f);
+    y = fmaf(y, m, 1.1676998740e-1f);
+    y = fmaf(y, m, -1.2420140846e-1f);
+    y = fmaf(y, m, 1.4249322787e-1f);
+    y = fmaf(y, m, -1.6668057665e-1f);
+    y = fmaf(y, m, 2.0000714765e-1f);
+    y = fmaf(y, m, -2.4999993993e-1f);
+    y = fmaf(y, m, 3.3333331174e-1f);
+    y = (y * m) * z;
+    const float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(-0.5f, z, y);
+    return fmaf(fe, 0.693359375f, m + y);
+}
+
+// Portable e^x for x in [-87, 0] (cephes expf; explicit fmaf).
+RT_HD float exp_pt(float x) {
+    const float z = floorf(x * 1.44269504088896341f + 0.5f);
+    float r = fmaf(-z, 0.693359375f, x);
+    r = fmaf(-z, -2.12194440e-4f, r);
+    float p = 1.9875691500e-4f;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    const float y = fmaf(p, r * r, r) + 1.0f;
+    return y * u2f((uint32_t)((int)z + 127) << 23);
+}
+
+// pow(x, y) for x in [0, 1], y > 0 (the gamma of drawTriangle, :702-703):
+// exp(y * log(x)); x <= 2^-100 gives 0 (the true value is < 2^-45).
+RT_HD float pow_pt(float x, float y) {
+    if (!(x > 7.88860905e-31f)) return 0.0f;
+    return exp_pt(y * log_pt(x));
+}
+
 }  // namespace rt

@@ -1,0 +1,359 @@
+// rt_mis.hip — gfx950 kernel of the MIS integrator: `kernel drawTriangle`
+// (Sources/gpuRaytracer/shaders.metal:635-707) with its one-bounce
+// three-strategy multiple importance sampling (`recursiveMultiImportanceSampling`,
+// :543-625): light-area, cosine-hemisphere and GGX-VNDF samples weighted by the
+// power heuristic with beta = 1 (:131-137), next-event estimation at the
+// secondary hit (:519-541), GGX/Lambert BRDF (:186-289).
+//
+// MI355X mapping:
+//   * one lane per pixel, wave64 = 8x8 pixel tile, 256-thread workgroups; the
+//     triangle records are staged in LDS once per workgroup (shared-edge pair
+//     layout, as in rt_kernel.hip) and every query is a closest hit with the
+//     wave-level AABB cull (rays of neighbouring pixels share u, so they are
+//     coherent);
+//   * the MIS sample points u do not depend on the pixel (haltonRandom(i, d),
+//     :556,564,584,595,617): the host tabulates them once per launch and the
+//     kernel reads them with wave-uniform (scalar) loads;
+//   * the tonemap epilogue (:688-706) is fused: one float4 and one uchar4 store.
+// Arithmetic follows DESIGN.md §3 / §3.11; oracle/pt_oracle.c (pto_render_mis)
+// restates the same operations and the two agree bit for bit.
+#include <hip/hip_runtime.h>
+
+#include "rt_kernel.hpp"
+#include "rt_trace.hpp"
+
+namespace rt {
+
+namespace {
+
+constexpr float kPiF = 3.14159274f;         // M_PI_F
+constexpr float kTwoPiF = 6.28318548f;      // 2.0 * M_PI_F
+constexpr float kInvPiF = 0.318309873f;     // 1.0 / M_PI_F (Fd_Lambert, :210-212)
+
+struct MisMat {
+    f3 diffuse;
+    float metallic, roughness;
+};
+
+struct MisHit {   // IntersectionGPU (:14-20) of a Hit
+    f3 p, n, din;  // point, normal, ray direction
+    MisMat m;
+};
+
+__device__ __forceinline__ float clamp01(float x) { return fminf(1.0f, fmaxf(0.0f, x)); }
+
+// D_GGX (:193-197): the caller passes roughness as `a`
+__device__ __forceinline__ float d_ggx(float NoH, float a) {
+    const float a2 = a * a;
+    const float f = (NoH * a2 - NoH) * NoH + 1.0f;
+    return a2 / ((kPiF * f) * f);
+}
+
+// smithG1_GGX (:186-191)
+__device__ __forceinline__ float smith_g1(float NoV, float roughness) {
+    const float a = roughness * roughness;
+    const float a2 = a * a;
+    const float NoV2 = NoV * NoV;
+    return 2.0f / (1.0f + sqrtf(1.0f + (a2 * (1.0f - NoV2)) / NoV2));
+}
+
+// V_SmithGGXCorrelated (:203-208)
+__device__ __forceinline__ float v_smith(float NoV, float NoL, float a) {
+    const float a2 = a * a;
+    const float GGXL = NoV * sqrtf(((-NoL) * a2 + NoL) * NoL + a2);
+    const float GGXV = NoL * sqrtf(((-NoV) * a2 + NoV) * NoV + a2);
+    return 0.5f / (GGXV + GGXL);
+}
+
+// calculateBRDFContribution (:259-289) for view ray direction din, light dir l
+__device__ __forceinline__ f3 brdf(f3 din, f3 n, const MisMat& m, f3 l) {
+    const f3 v = -normalize(din);
+    const f3 h = normalize(v + l);
+    const float NoV = fabsf(dot(n, v)) + 1e-5f;
+    const float NoL = clamp01(dot(n, l));
+    const float NoH = clamp01(dot(n, h));
+    const float LoH = clamp01(dot(l, h));
+    // f0 = mix(0.04, diffuse, metallic) = 0.04 + (diffuse - 0.04) * metallic
+    const f3 f0{0.04f + (m.diffuse.x - 0.04f) * m.metallic, 0.04f + (m.diffuse.y - 0.04f) * m.metallic,
+                0.04f + (m.diffuse.z - 0.04f) * m.metallic};
+    const float D = d_ggx(NoH, m.roughness);
+    const float x = 1.0f - LoH;
+    const float x2 = x * x;
+    const float p5 = (x2 * x2) * x;  // pow(1 - LoH, 5.0)
+    const f3 F{f0.x + (1.0f - f0.x) * p5, f0.y + (1.0f - f0.y) * p5, f0.z + (1.0f - f0.z) * p5};
+    const float G = v_smith(NoV, NoL, m.roughness);
+    const float DG = D * G;
+    const float den = (4.0f * NoV) * NoL + 1e-7f;
+    const f3 Fr{(DG * F.x) / den, (DG * F.y) / den, (DG * F.z) / den};
+    const f3 Fd = m.diffuse * kInvPiF;
+    const float km = 1.0f - m.metallic;
+    const f3 kD{(1.0f - F.x) * km, (1.0f - F.y) * km, (1.0f - F.z) * km};
+    return (kD * (Fd + Fr)) * NoL;
+}
+
+// calculateVNDFPdf (:437-445)
+__device__ __forceinline__ float vndf_pdf(f3 V, f3 n, f3 L, float roughness) {
+    const f3 h = normalize(V + L);
+    const float NoH = fabsf(dot(n, h));
+    const float VoH = fabsf(dot(V, h));
+    const float NoV = fabsf(dot(n, V));
+    const float D = d_ggx(NoH, roughness);
+    const float G1 = smith_g1(NoV, roughness);
+    return ((D * G1) * VoH) / (4.0f * NoV);
+}
+
+// calculateCosineWeightedPdf (:376-380)
+__device__ __forceinline__ float cosine_pdf(f3 n, f3 d) { return fmaxf(0.0f, dot(n, d)) / kPiF; }
+
+// calculateSquareLightPdf (:315-326): evaluated at the un-offset hit point
+__device__ __forceinline__ float light_pdf(const MisParams& P, f3 p, f3 d) {
+    const f3 toL = f3{P.l_center[0], P.l_center[1], P.l_center[2]} - p;
+    const float dist = length(toL);
+    const float cosT = fmaxf(0.0f, dot(-d, f3{0.0f, -1.0f, 0.0f}));
+    return (dist * dist) / (P.l_area * cosT + 1e-6f);
+}
+
+// powerHeuristic with beta = 1 (:132-137; pow(x, 1) = x)
+__device__ __forceinline__ float power_h(float p1, float p2, float p3, float n) {
+    const float a = n * p1;
+    const float sum = (a + n * p2) + n * p3;
+    return a / (sum + 1e-6f);
+}
+
+// cosineWeightedRay direction (:355-374)
+__device__ __forceinline__ f3 cosine_dir(f3 n, f3 t, f3 b, float ux, float uy) {
+    const float phi = kTwoPiF * ux;
+    const float cosT = sqrtf(uy);
+    const float sinT = sqrtf(1.0f - uy);
+    float sp, cp;
+    sincos_pt(phi, &sp, &cp);
+    return normalize((t * (cp * sinT) + b * (sp * sinT)) + n * cosT);
+}
+
+// vndfRay direction (:382-435); V = -ray direction of the hit
+__device__ __forceinline__ f3 vndf_dir(f3 V, f3 n, f3 t, f3 b, float roughness, float ux, float uy) {
+    const float alpha = roughness * roughness;
+    const f3 Ve = normalize(f3{alpha * dot(V, t), alpha * dot(V, b), dot(V, n)});
+    const f3 T1 = normalize(f3{Ve.z, 0.0f, -Ve.x});
+    const f3 T2 = cross(Ve, T1);
+    const float phi = kTwoPiF * ux;
+    const float lenVe = length(Ve);
+    const float ctm = lenVe / sqrtf(1.0f + lenVe * lenVe);
+    const float ct = ctm + (1.0f - ctm) * uy;
+    const float st = sqrtf(1.0f - ct * ct);
+    float sp, cp;
+    sincos_pt(phi, &sp, &cp);
+    const f3 h = normalize((T1 * (cp * st) + T2 * (sp * st)) + Ve * ct);
+    const f3 Nh = normalize(f3{alpha * h.x, alpha * h.y, fmaxf(0.0f, h.z)});
+    const f3 wH = normalize((t * Nh.x + b * Nh.y) + n * Nh.z);
+    const f3 I = -V;
+    return I - wH * (2.0f * dot(wH, I));  // reflect(-V, wH)
+}
+
+__device__ __forceinline__ MisMat load_mat(const float4* rec) {
+    const float4 r1 = rec[1], r2 = rec[2];
+    return MisMat{f3{r1.x, r1.y, r1.z}, r1.w, r2.x};
+}
+
+template <int GEO>
+__device__ __forceinline__ int mis_closest(const SceneView& sv, f3 o, f3 d, float tmax, float* t) {
+    *t = tmax;
+    return closest_hit<GEO, false, true, 0>(sv, o, d, 0.001f, t);
+}
+
+// calculateDirectLightSamplingContribution (:519-541).  POWER: MIS-weighted
+// (first hit) or plain (at the secondary hit, samplesPerStrategy = 1).
+template <int GEO, bool POWER>
+__device__ __forceinline__ f3 direct_light(const MisParams& P, const SceneView& sv, const MisHit& x,
+                                           float ux, float uy, float nS) {
+    const f3 origin = x.p + x.n * 1e-4f;
+    // directSquareLightRay (:291-313)
+    const float sx = (ux - 0.5f) * P.l_width;
+    const float sy = (uy - 0.5f) * P.l_depth;
+    const f3 sp = (f3{P.l_center[0], P.l_center[1], P.l_center[2]} +
+                   f3{P.l_tangent[0], P.l_tangent[1], P.l_tangent[2]} * sx) +
+                  f3{P.l_bitangent[0], P.l_bitangent[1], P.l_bitangent[2]} * sy;
+    const f3 tl = sp - origin;
+    const float dist = length(tl);
+    const f3 L{tl.x / dist, tl.y / dist, tl.z / dist};
+    float t;
+    const int id = mis_closest<GEO>(sv, origin, L, dist, &t);
+    if (id < 0 || P.mis_shade[3 * id].w == 0.0f) return f3{0.0f, 0.0f, 0.0f};  // not HitLight
+    const float dl_pdf = light_pdf(P, x.p, L);
+    const f3 c = brdf(x.din, x.n, x.m, L);
+    const f3 Le{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
+    if (POWER) {
+        const float cos_pdf = cosine_pdf(x.n, L);
+        const float v_pdf = vndf_pdf(-x.din, x.n, L, x.m.roughness);
+        const float w = power_h(dl_pdf, cos_pdf, v_pdf, nS);
+        const f3 a = (c * w) * Le;
+        return f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
+    }
+    const f3 a = c * Le;
+    return f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
+}
+
+// Continuation of a cosine or VNDF sample (:576-590, :608-622): the sampled
+// ray's closest hit either sees the light (MIS-weighted emission) or a
+// surface (next-event estimate there, unweighted).
+template <int GEO>
+__device__ __forceinline__ f3 continue_sample(const MisParams& P, const SceneView& sv,
+                                              const MisHit& x, f3 origin, f3 dir, float pdf,
+                                              float w, float u2x, float u2y) {
+    float t;
+    const int id = mis_closest<GEO>(sv, origin, dir, 1000.0f, &t);
+    if (id < 0) return f3{0.0f, 0.0f, 0.0f};
+    const float4* rec = P.mis_shade + 3 * id;
+    const float4 r0 = rec[0];
+    const f3 c = brdf(x.din, x.n, x.m, dir);
+    if (r0.w != 0.0f) {  // HitLight
+        const f3 a = (c * w) * f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
+        return f3{a.x / pdf, a.y / pdf, a.z / pdf};
+    }
+    MisHit y;
+    y.p = origin + dir * t;
+    y.n = f3{r0.x, r0.y, r0.z};
+    y.din = dir;
+    y.m = load_mat(rec);
+    const f3 q{c.x / pdf, c.y / pdf, c.z / pdf};
+    return q * direct_light<GEO, false>(P, sv, y, u2x, u2y, 1.0f);
+}
+
+// recursiveMultiImportanceSampling (:543-625)
+template <int GEO>
+__device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView& sv,
+                                            const MisHit& x) {
+    const uint32_t S = P.S;
+    const float nS = (float)S;
+    const float4* __restrict__ tab = P.u_tab;
+    f3 dl{0.0f, 0.0f, 0.0f}, cs{0.0f, 0.0f, 0.0f}, vn{0.0f, 0.0f, 0.0f};
+    for (uint32_t i = 0; i < S; ++i) {  // light sampling (:553-560)
+        const float4 u = tab[3 * i];
+        dl = dl + direct_light<GEO, true>(P, sv, x, u.x, u.y, nS);
+    }
+    f3 t, b;
+    onb(x.n, &t, &b);
+    const f3 origin = x.p + x.n * 1e-4f;
+    const f3 V = -x.din;
+    for (uint32_t i = 0; i < S; ++i) {  // cosine-hemisphere sampling (:562-591)
+        const float4 u = tab[3 * i + 1];
+        const f3 dir = cosine_dir(x.n, t, b, u.x, u.y);
+        const float cos_pdf = cosine_pdf(x.n, dir);
+        const float dl_pdf = light_pdf(P, x.p, dir);
+        const float v_pdf = vndf_pdf(V, x.n, dir, x.m.roughness);
+        const float w = power_h(cos_pdf, dl_pdf, v_pdf, nS);
+        cs = cs + continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w);
+    }
+    for (uint32_t i = 0; i < S; ++i) {  // VNDF sampling (:593-623)
+        const float4 u = tab[3 * i + 2];
+        const f3 dir = vndf_dir(V, x.n, t, b, x.m.roughness, u.x, u.y);
+        const float v_pdf = vndf_pdf(V, x.n, dir, x.m.roughness);
+        const float cos_pdf = cosine_pdf(x.n, dir);
+        const float dl_pdf = light_pdf(P, x.p, dir);
+        const float w = power_h(v_pdf, dl_pdf, cos_pdf, nS);
+        vn = vn + continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w);
+    }
+    const f3 sum = (dl + cs) + vn;
+    return f3{sum.x / nS, sum.y / nS, sum.z / nS};
+}
+
+}  // namespace
+
+template <int GEO>
+__global__ __launch_bounds__(kBlockThreads) void mis_kernel(MisParams P) {
+    extern __shared__ float4 lds[];
+    SceneView sv;
+    sv.nT = P.nT;
+    sv.nP = P.nP;
+    sv.nS = 0;
+    sv.nN = 0;
+    sv.node = nullptr;
+    sv.sph = nullptr;
+    sv.sph_perm = nullptr;
+    if (GEO != kGeoTriGlobal) {
+        const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
+        const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
+        for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
+        __syncthreads();
+        sv.tri = lds;
+        sv.pair = lds;
+    } else {
+        sv.tri = P.tri_isect;
+        sv.pair = nullptr;
+    }
+
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t j = blockIdx.y * kTile + (wave >> 1) * 8u + (lane >> 3);
+    if (x >= (uint32_t)P.W || j >= P.row_count) return;
+    const uint32_t y = P.row_start + j * P.row_step;
+    const size_t o = (size_t)j * (size_t)P.W + x;
+
+    const f3 cu{P.cam_u[0], P.cam_u[1], P.cam_u[2]}, cv{P.cam_v[0], P.cam_v[1], P.cam_v[2]};
+    const f3 cw{P.cam_w[0], P.cam_w[1], P.cam_w[2]};
+    const f3 cpos{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
+    const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
+    f3 acc{0.0f, 0.0f, 0.0f};
+    for (uint32_t i = 0; i < P.camera_rays; ++i) {  // :652
+        // hashRandom(index, i) (:71-85); the 800 is the reference's hard-coded width
+        const uint32_t sample_id = (y * 800u + x) * i;
+        const float jx = mis_unit(mis_hash(x + y * 800u + sample_id));
+        const float jy = mis_unit(mis_hash(y + x * 600u + sample_id + 12345u));
+        // generateCameraRay (:214-246)
+        const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
+        const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
+        const float sh = sx * P.halfW, th = ty * P.halfH;
+        const f3 d = normalize((cu * sh + cv * th) - cw);
+        float t;
+        const int id = mis_closest<GEO>(sv, cpos, d, 1000.0f, &t);
+        if (id < 0) continue;                               // Miss (:665)
+        const float4* rec = P.mis_shade + 3 * id;
+        const float4 r0 = rec[0];
+        if (r0.w != 0.0f) {                                 // HitLight (:667-671)
+            acc = acc + f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
+            continue;
+        }
+        MisHit h;
+        h.p = cpos + d * t;
+        h.n = f3{r0.x, r0.y, r0.z};
+        h.din = d;
+        h.m = load_mat(rec);
+        acc = acc + mis_shade_hit<GEO>(P, sv, h);           // :674-676
+    }
+    const float nc = (float)P.camera_rays;
+    if (P.out) P.out[o] = make_float4(acc.x, acc.y, acc.z, nc);  // textBuffer (:705) + count
+    if (P.out8) {
+        // :688-706: exposure, Reinhard, clamp, gamma 1/2.2, uchar(c * 255)
+        const float e[3] = {(acc.x / nc) * P.exposure, (acc.y / nc) * P.exposure,
+                            (acc.z / nc) * P.exposure};
+        unsigned char c8[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float tm = clamp01(e[k] / (e[k] + 1.0f));
+            const float g = pow_pt(tm, 1.0f / 2.2f);
+            c8[k] = (unsigned char)(g * 255.0f);
+        }
+        P.out8[o] = make_uchar4(c8[0], c8[1], c8[2], 255);
+    }
+}
+
+size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {
+    return (size_t)(n_pairs ? kPairF4 * n_pairs : 3u * n_tri) * sizeof(float4);
+}
+
+hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
+    const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
+    const bool pairs = mem != SceneMem::kLdsSingle && P.nP > 0;
+    const size_t lds = mis_lds_bytes(P.nT, pairs ? P.nP : 0u);
+    if (mem != SceneMem::kSmem && lds <= kMaxLdsBytes) {
+        if (pairs)
+            hipLaunchKernelGGL(mis_kernel<kGeoPairLds>, grid, dim3(kBlockThreads), lds, stream, P);
+        else
+            hipLaunchKernelGGL(mis_kernel<kGeoTriLds>, grid, dim3(kBlockThreads), lds, stream, P);
+    } else {
+        hipLaunchKernelGGL(mis_kernel<kGeoTriGlobal>, grid, dim3(kBlockThreads), 0, stream, P);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rt

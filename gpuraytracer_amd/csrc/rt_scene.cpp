@@ -123,7 +123,7 @@ std::vector<Triangle> create_cornell_box_scene() {
     return t;
 }
 
-Scene init_cornell_box(int32_t width, int32_t height) {
+static Scene cornell_box(int32_t width, int32_t height, float light_size) {
     Scene s;
     s.camera.position = f3{0, 0, 9};
     s.camera.direction = normalize(f3{0, 0, -2.5f} - f3{0, 0, 9});
@@ -134,7 +134,7 @@ Scene init_cornell_box(int32_t width, int32_t height) {
     s.camera.ev100 = 5.0f;
 
     const float half = 5.0f / 2.0f;
-    const float light_w = 1.0f, light_d = 1.0f;
+    const float light_w = light_size, light_d = light_size;
     const float light_y = half - 0.01f;
     const f3 lc{0, light_y, 0};
     const float hw = light_w / 2, hd = light_d / 2;
@@ -155,6 +155,10 @@ Scene init_cornell_box(int32_t width, int32_t height) {
     s.triangles.push_back(Triangle{{v0, v2, v3}, light_m});
     return s;
 }
+
+Scene init_cornell_box(int32_t width, int32_t height) { return cornell_box(width, height, 1.0f); }
+
+Scene init_cornell_box_mis(int32_t width, int32_t height) { return cornell_box(width, height, 1.5f); }
 
 Scene init_random_spheres(int32_t width, int32_t height, uint32_t n, uint64_t seed) {
     Scene s = init_cornell_box(width, height);
@@ -463,6 +467,32 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                              light_flag, em.x, em.y, em.z, 0.0f,
                              sp.center.x, sp.center.y, sp.center.z, sp.radius * sp.radius};
         memcpy(out->sph_shade[k].s, s, sizeof(s));
+    }
+    // MIS integrator records (Sources/gpuRaytracer/shaders.metal)
+    out->mis_shade.resize(n_tri);
+    for (uint32_t k = 0; k < n_tri; ++k) {
+        const float* ts = out->tri_shade[k].s;  // (N.xyz, light) first
+        const float s[12] = {ts[0], ts[1], ts[2], ts[3],
+                             mats[k].diffuse.x, mats[k].diffuse.y, mats[k].diffuse.z, mats[k].metallic,
+                             mats[k].roughness, 0.0f, 0.0f, 0.0f};
+        memcpy(out->mis_shade[k].s, s, sizeof(s));
+    }
+    MisLightConst& ml = out->mis_light;
+    f3 t, b;
+    onb(f3{0.0f, -1.0f, 0.0f}, &t, &b);  // directSquareLightRay (:292-293)
+    const float c3[3] = {light.center.x, light.center.y, light.center.z};
+    const float t3[3] = {t.x, t.y, t.z}, b3[3] = {b.x, b.y, b.z};
+    const float r3[3] = {light.emittedRadiance.x, light.emittedRadiance.y, light.emittedRadiance.z};
+    memcpy(ml.center, c3, sizeof(c3));
+    memcpy(ml.tangent, t3, sizeof(t3));
+    memcpy(ml.bitangent, b3, sizeof(b3));
+    memcpy(ml.radiance, r3, sizeof(r3));
+    ml.width = light.width;
+    ml.depth = light.depth;
+    ml.area = light.width * light.depth;  // calculateSquareLightPdf (:323)
+    {
+        volatile float ev = cam.ev100;     // run-time libm (never constant folded)
+        ml.exposure = 1.0f / (1.2f * powf(2.0f, ev));
     }
     return true;
 }

@@ -70,6 +70,21 @@ struct LightConst {
     float center[3], color[3];
 };
 
+// Square light as the MIS integrator uses it (Sources/gpuRaytracer/
+// shaders.metal:291-326): basis of the hard-coded normal (0,-1,0), size and
+// emittedRadiance.  Computed once per scene with the contract ops.
+struct MisLightConst {
+    float center[3], tangent[3], bitangent[3], radiance[3];
+    float width, depth, area;
+    float exposure;  // cameraExposure (shaders.metal:145-150), host libm powf
+};
+
+// Per-triangle record of the MIS integrator, 48 B:
+// (N.xyz, light), (diffuse.rgb, metallic), (roughness, 0, 0, 0)
+struct MisShade {
+    float s[12];
+};
+
 struct CompiledScene {
     CamConst cam;
     LightConst light;
@@ -80,6 +95,8 @@ struct CompiledScene {
     std::vector<uint32_t> sph_perm;     // leaf-order index -> sphere id (shading, ties)
     std::vector<BvhNode> sph_nodes;
     std::vector<SphShade> sph_shade;    // by sphere id
+    MisLightConst mis_light;
+    std::vector<MisShade> mis_shade;    // by triangle id
 };
 
 // Validates and precomputes; returns false with *err set on bad input.
@@ -129,6 +146,8 @@ struct Scene {  // scene.swift:8-12 (+ spheres for config 4)
 };
 
 Scene init_cornell_box(int32_t width, int32_t height);                  // scene.swift:14-62
+// Sources/gpuRaytracer/main.swift:21-67: the same room with a 1.5 x 1.5 light
+Scene init_cornell_box_mis(int32_t width, int32_t height);
 std::vector<Triangle> create_cornell_box_scene();                       // scene.swift:64-175
 Scene init_random_spheres(int32_t width, int32_t height, uint32_t n, uint64_t seed);
 

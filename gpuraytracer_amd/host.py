@@ -18,8 +18,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from ._native import (RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE,
-                      CameraGPU, MaterialGPU, RenderParamsC, RtError, SceneDesc, SceneInfo,
-                      SphereGPU, SquareLightGPU, float3, lib)
+                      CameraGPU, MaterialGPU, MisParamsC, RenderParamsC, RtError, SceneDesc,
+                      SceneInfo, SphereGPU, SquareLightGPU, float3, lib)
 
 DEFAULT_SEED_KEY = 0x5EED00000000
 
@@ -89,6 +89,19 @@ class Scene:
         return cls(cam, mats, verts, light)
 
     @classmethod
+    def cornell_box_mis(cls, width: int = 800, height: int = 600) -> "Scene":
+        """The SwiftPM build's scene (Sources/gpuRaytracer/main.swift:21-67):
+        the same room with a 1.5 x 1.5 light."""
+        cam, light = CameraGPU(), SquareLightGPU()
+        mats = (MaterialGPU * 36)()
+        verts = (float3 * 108)()
+        n = ctypes.c_uint32()
+        _check(lib.rt_scene_cornell_box_mis(width, height, ctypes.byref(cam), mats, verts,
+                                            ctypes.byref(light), ctypes.byref(n)))
+        assert n.value == 36
+        return cls(cam, mats, verts, light)
+
+    @classmethod
     def random_spheres(cls, width: int = 1920, height: int = 1080, n_spheres: int = 1000,
                        seed: int = 42) -> "Scene":
         """Config-4 scene: Cornell walls + light + PCG32(seed) spheres."""
@@ -150,6 +163,28 @@ class RenderParams:
             return self.row_count
         step = self.row_step or 1
         return (height - 1 - self.row_start) // step + 1
+
+
+@dataclass
+class MisParams:
+    """rt_mis_params (include/rtpt.h): kernel drawTriangle of the SwiftPM build."""
+
+    camera_rays: int = 6    # cameraRaysPerPixel, Sources/gpuRaytracer/shaders.metal:644
+    mis_samples: int = 300  # misSamples, :648
+    row_start: int = 0
+    row_step: int = 1
+    row_count: int = 0
+
+    def c(self, flags: int = 0) -> MisParamsC:
+        p = MisParamsC()
+        p.camera_rays, p.mis_samples = self.camera_rays, self.mis_samples
+        p.row_start, p.row_step, p.row_count = self.row_start, self.row_step, self.row_count
+        p.flags = flags
+        return p
+
+    def rows(self, height: int) -> int:
+        return RenderParams(row_start=self.row_start, row_step=self.row_step,
+                            row_count=self.row_count).rows(height)
 
 
 class Renderer:
@@ -221,6 +256,25 @@ class Renderer:
     def draw(self, spp: int = 400, bounces: int = 3) -> np.ndarray:
         """Renderer.draw(): the whole frame, synchronously; (H, W, 4) float32."""
         return self.render(RenderParams(spp=spp, bounces=bounces))
+
+    def render_mis(self, params: MisParams | None = None, out=None, out8=None):
+        """MIS integrator (rt_render_mis).  Host: returns (sum, rgba8) with
+        sum (rows, W, 4) float32 = (radiance summed over camera rays, camera
+        rays) and rgba8 (rows, W, 4) uint8.  Device: pass tensors ``out`` and/or
+        ``out8`` (anything with ``data_ptr()``); the call is synchronous."""
+        p = params or MisParams()
+        if out is None and out8 is None:
+            rows = p.rows(self.scene.height)
+            img = np.empty((rows, self.scene.width, 4), dtype=np.float32)
+            img8 = np.empty((rows, self.scene.width, 4), dtype=np.uint8)
+            _check(lib.rt_render_mis(self._ctx, ctypes.byref(p.c()),
+                                     img.ctypes.data_as(ctypes.c_void_p),
+                                     img8.ctypes.data_as(ctypes.c_void_p)), self._ctx)
+            return img, img8
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())  # noqa: E731
+        _check(lib.rt_render_mis(self._ctx, ctypes.byref(p.c(RT_OUT_DEVICE)), ptr(out), ptr(out8)),
+               self._ctx)
+        return out, out8
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()

@@ -148,6 +148,35 @@ int rt_scene_random_spheres(int32_t width, int32_t height, uint32_t n_spheres,
                             rt_float3* vertices, SquareLightGPU* light,
                             uint32_t* n_triangles, SphereGPU* spheres);
 
+/* ---- MIS integrator ----------------------------------------------------
+ * The SwiftPM build's kernel `drawTriangle` (Sources/gpuRaytracer/shaders.metal:
+ * 635-707, bound at Sources/gpuRaytracer/computeShader.swift:99-189): per pixel
+ * `camera_rays` hash-jittered camera rays; a camera ray that hits the light
+ * adds light.emittedRadiance, a surface hit adds the one-bounce three-strategy
+ * MIS estimate of recursiveMultiImportanceSampling (:543-625) with
+ * samplesPerStrategy = mis_samples / 3.  Triangle scenes only. */
+typedef struct rt_mis_params {
+    uint32_t camera_rays;   /* cameraRaysPerPixel (:644), reference 6 */
+    uint32_t mis_samples;   /* misSamples (:648), reference 300 */
+    uint32_t row_start, row_step, row_count;  /* as rt_render_params */
+    uint32_t flags;         /* RT_OUT_DEVICE: both outputs are device pointers */
+} rt_mis_params;
+
+/* out_rgba32f (optional): (sum of the camera-ray radiances, camera_rays) per
+ *   pixel, row_count*W float4 -- the reference's textBuffer (:627-633,705)
+ *   plus the divisor.
+ * out_rgba8 (optional): the reference's pixels (:248-257,688-706): exposure
+ *   1/(1.2*2^ev100), Reinhard, clamp, gamma 1/2.2, uchar(c*255), alpha 255.
+ * At least one output must be non-null.  Synchronous. */
+int rt_render_mis(rt_ctx* ctx, const rt_mis_params* params, float* out_rgba32f,
+                  uint8_t* out_rgba8);
+
+/* The SwiftPM scene (Sources/gpuRaytracer/main.swift:21-67, :96-173): the
+ * RTrace room with a 1.5 x 1.5 light.  Arrays as rt_scene_cornell_box. */
+int rt_scene_cornell_box_mis(int32_t width, int32_t height, CameraGPU* camera,
+                             MaterialGPU* materials, rt_float3* vertices,
+                             SquareLightGPU* light, uint32_t* n_triangles);
+
 /* How rt_create would lay a scene out on the device (host-only, no device). */
 typedef struct rt_scene_info {
     uint32_t n_triangles;

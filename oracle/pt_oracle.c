@@ -112,6 +112,7 @@ typedef struct {
     v3 v0, e1, e2, n;    /* n = cross(e1,e2): unnormalized geometric normal      */
     v3 N, right, fwd;    /* getTriangleNormal (sampling.metal:16-26) + frame     */
     v3 diffuse, emissive;
+    float metallic, roughness;  /* MIS integrator only (Sources/.../shaders.metal) */
     int light;           /* length(emissive) > 0 (raytrace.metal:57)              */
 } tri_t;
 
@@ -198,6 +199,8 @@ static int scene_build(scene_t* s, const CameraGPU* cam, const MaterialGPU* mats
         frame_of(T->N, &T->right, &T->fwd);
         T->diffuse = mk(mats[k].diffuse.x, mats[k].diffuse.y, mats[k].diffuse.z);
         T->emissive = ld3(&mats[k].emissive);
+        T->metallic = mats[k].metallic;
+        T->roughness = mats[k].roughness;
         T->light = is_light(T->emissive);
     }
     for (uint32_t k = 0; k < nS; ++k) {
@@ -513,8 +516,8 @@ static const int kBoxFaces[12][3] = {{0, 2, 1}, {0, 3, 2}, {4, 5, 6}, {4, 6, 7},
                                      {0, 4, 7}, {0, 7, 3}, {1, 6, 5}, {1, 2, 6},
                                      {0, 5, 4}, {0, 1, 5}, {3, 6, 2}, {3, 7, 6}};
 
-int pto_cornell_box(int32_t width, int32_t height, CameraGPU* cam, MaterialGPU* mats,
-                    rt_float3* verts, SquareLightGPU* light, uint32_t* n_tri) {
+static int cornell(int32_t width, int32_t height, float lsize, CameraGPU* cam, MaterialGPU* mats,
+                   rt_float3* verts, SquareLightGPU* light, uint32_t* n_tri) {
     if (!cam || !mats || !verts || !light || width <= 0 || height <= 0) return -1;
     memset(cam, 0, sizeof(*cam));
     /* scene.swift:16-18; Camera defaults :290-296 */
@@ -531,7 +534,7 @@ int pto_cornell_box(int32_t width, int32_t height, CameraGPU* cam, MaterialGPU* 
 
     const float half = 5.0f / 2.0f; /* :20-21 */
     const float lightY = half - 0.01f;
-    const float hw = 1.0f / 2, hd = 1.0f / 2;
+    const float hw = lsize / 2, hd = lsize / 2;
     const rt_float3 L0 = f3(0 - hw, lightY, 0 - hd), L1 = f3(0 + hw, lightY, 0 - hd);
     const rt_float3 L2 = f3(0 + hw, lightY, 0 + hd), L3 = f3(0 - hw, lightY, 0 + hd);
     const MaterialGPU lightM = material(1.0f, 0.95f, 0.9f, 0.0f, 0.0f, 1, 1, 1); /* :37-43 */
@@ -576,13 +579,24 @@ int pto_cornell_box(int32_t width, int32_t height, CameraGPU* cam, MaterialGPU* 
     light->color = lightM.diffuse;
     {
         const float flux = 100.0f * 12.0f;
-        const float area = 1.0f * 1.0f;
+        const float area = lsize * lsize;
         const float lum = (flux / area) / kSwiftPi;
         light->emittedRadiance = f3(1.0f * lum, 0.95f * lum, 0.9f * lum);
     }
-    light->width = 1.0f;
-    light->depth = 1.0f;
+    light->width = lsize;
+    light->depth = lsize;
     return 0;
+}
+
+int pto_cornell_box(int32_t width, int32_t height, CameraGPU* cam, MaterialGPU* mats,
+                    rt_float3* verts, SquareLightGPU* light, uint32_t* n_tri) {
+    return cornell(width, height, 1.0f, cam, mats, verts, light, n_tri);
+}
+
+/* Sources/gpuRaytracer/main.swift:21-67: lightWidth = lightDepth = 1.5 */
+int pto_cornell_box_mis(int32_t width, int32_t height, CameraGPU* cam, MaterialGPU* mats,
+                        rt_float3* verts, SquareLightGPU* light, uint32_t* n_tri) {
+    return cornell(width, height, 1.5f, cam, mats, verts, light, n_tri);
 }
 
 /* PCG32 (O'Neill), srandom(initstate=seed, initseq=54) */
@@ -711,4 +725,408 @@ void pto_tonemap_rgba8(const float* in, size_t n, uint8_t* out) {
         }
         out[4 * i + 3] = 255;
     }
+}
+
+
+/* ========================================================================
+ * MIS integrator: kernel drawTriangle of the SwiftPM build
+ * (Sources/gpuRaytracer/shaders.metal:635-707) and its helpers, restated
+ * under the same contract.  Every line cites the
+ * reference statement it follows.
+ * ======================================================================== */
+
+static const float kPiF = 3.14159274f;      /* M_PI_F */
+static const float kInvPiF = 0.318309873f;  /* 1.0 / M_PI_F, Fd_Lambert :210-212 */
+
+static float c01(float x) { return fminf(1.0f, fmaxf(0.0f, x)); }
+static v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+
+/* hash, randomFloat, hashRandom (:58-85) */
+static uint32_t mis_hash(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+static float random_float(uint32_t seed) {
+    /* float(hash) / (float(0xffffffffU) + 1.0): the denominator is 2^32 in
+     * float, so the quotient is the exact product below */
+    return (float)mis_hash(seed) * 2.3283064365386963e-10f;
+}
+
+/* buildOrthonormalBasis (:159-172) */
+static void mis_onb(v3 n, v3* t, v3* b) {
+    v3 a;
+    if (fabsf(n.x) > 0.9f) a = mk(0.0f, 1.0f, 0.0f);
+    else a = mk(1.0f, 0.0f, 0.0f);
+    *t = nrm(sub(a, scl(n, dot(a, n))));
+    *b = cross(n, *t);
+}
+
+/* D_GGX, F_Schlick, V_SmithGGXCorrelated, smithG1_GGX (:186-208) */
+static float d_ggx(float NoH, float a) {
+    const float a2 = a * a;
+    const float f = (NoH * a2 - NoH) * NoH + 1.0f;
+    return a2 / (kPiF * f * f);
+}
+static float pow5(float x) { const float x2 = x * x; return (x2 * x2) * x; } /* DESIGN §3.11 */
+static v3 f_schlick(float LoH, v3 f0) {
+    const float p = pow5(1.0f - LoH);
+    return mk(f0.x + (1.0f - f0.x) * p, f0.y + (1.0f - f0.y) * p, f0.z + (1.0f - f0.z) * p);
+}
+static float v_smith(float NoV, float NoL, float a) {
+    const float a2 = a * a;
+    const float GGXL = NoV * sqrtf((-NoL * a2 + NoL) * NoL + a2);
+    const float GGXV = NoL * sqrtf((-NoV * a2 + NoV) * NoV + a2);
+    return 0.5f / (GGXV + GGXL);
+}
+static float smith_g1(float NoV, float roughness) {
+    const float a = roughness * roughness;
+    const float a2 = a * a;
+    const float NoV2 = NoV * NoV;
+    return 2.0f / (1.0f + sqrtf(1.0f + a2 * (1.0f - NoV2) / NoV2));
+}
+
+typedef enum { MIS_HIT, MIS_HIT_LIGHT, MIS_MISS } mis_type;
+typedef struct {          /* IntersectionGPU (:14-20) */
+    mis_type type;
+    v3 point;
+    v3 ro, rd;            /* ray */
+    v3 normal;
+    const tri_t* mat;     /* material (diffuse, metallic, roughness) */
+} mis_isect;
+
+typedef struct {
+    v3 center, tangent, bitangent, radiance;
+    float width, depth;
+} mis_light;
+
+/* getClosestIntersection (:459-509), rays in (min, max) per DESIGN.md §3.5 */
+static mis_isect closest_isect(const scene_t* s, v3 o, v3 d, float tmin, float tmax) {
+    mis_isect r;
+    memset(&r, 0, sizeof(r));
+    float t;
+    const int id = closest(s, o, d, tmin, tmax, &t);
+    if (id < 0) { r.type = MIS_MISS; return r; }
+    const tri_t* T = &s->tris[id];
+    r.point = add(o, scl(d, t));
+    r.mat = T;
+    if (T->light) { r.type = MIS_HIT_LIGHT; return r; }
+    r.type = MIS_HIT;
+    r.ro = o;
+    r.rd = d;
+    r.normal = T->N;  /* getTriangleNormal (:447-457) */
+    return r;
+}
+
+/* calculateBRDFContribution (:259-289) */
+static v3 brdf(v3 ray_d, v3 n, const tri_t* m, v3 l) {
+    const v3 v = neg(nrm(ray_d));
+    const v3 h = nrm(add(v, l));
+    const float NoV = fabsf(dot(n, v)) + 1e-5f;
+    const float NoL = c01(dot(n, l));
+    const float NoH = c01(dot(n, h));
+    const float LoH = c01(dot(l, h));
+    const v3 f0 = mk(0.04f + (m->diffuse.x - 0.04f) * m->metallic,   /* mix(0.04, diffuse, metallic) */
+                     0.04f + (m->diffuse.y - 0.04f) * m->metallic,
+                     0.04f + (m->diffuse.z - 0.04f) * m->metallic);
+    const float D = d_ggx(NoH, m->roughness);
+    const v3 F = f_schlick(LoH, f0);
+    const float G = v_smith(NoV, NoL, m->roughness);
+    const float den = 4.0f * NoV * NoL + 1e-7f;
+    const v3 Fr = divs(scl(F, D * G), den);
+    const v3 Fd = scl(m->diffuse, kInvPiF);
+    const v3 kD = scl(sub(mk(1.0f, 1.0f, 1.0f), F), 1.0f - m->metallic);
+    return scl(mul(kD, add(Fd, Fr)), NoL);
+}
+
+/* calculateSquareLightPdf (:315-326) */
+static float light_pdf(const mis_light* L, v3 origin, v3 dir) {
+    const v3 toL = sub(L->center, origin);
+    const float dist = len(toL);
+    const float cosT = fmaxf(0.0f, dot(neg(dir), mk(0.0f, -1.0f, 0.0f)));
+    const float area = L->width * L->depth;
+    return (dist * dist) / (area * cosT + 1e-6f);
+}
+
+/* calculateCosineWeightedPdf (:376-380) */
+static float cosine_pdf(v3 n, v3 d) { return fmaxf(0.0f, dot(n, d)) / kPiF; }
+
+/* calculateVNDFPdf (:437-445) */
+static float vndf_pdf(v3 V, v3 n, v3 L, float roughness) {
+    const v3 h = nrm(add(V, L));
+    const float NoH = fabsf(dot(n, h));
+    const float VoH = fabsf(dot(V, h));
+    const float NoV = fabsf(dot(n, V));
+    const float D = d_ggx(NoH, roughness);
+    const float G1 = smith_g1(NoV, roughness);
+    return (D * G1 * VoH) / (4.0f * NoV);
+}
+
+/* powerHeuristic, beta = 1 (:132-137): pow(x, 1) = x */
+static float power_h(float p1, float p2, float p3, uint32_t spp) {
+    const float n = (float)spp;
+    const float a = n * p1;
+    const float sum = a + n * p2 + n * p3;
+    return a / (sum + 1e-6f);
+}
+
+/* cosineWeightedRay (:355-374): direction */
+static v3 cosine_ray_dir(v3 n, float ux, float uy) {
+    const float phi = 2.0f * kPiF * ux;
+    const float cosT = sqrtf(uy);
+    const float sinT = sqrtf(1.0f - uy);
+    v3 t, b;
+    mis_onb(n, &t, &b);
+    float sp, cp;
+    pto_sincos(phi, &sp, &cp);
+    return nrm(add(add(scl(t, cp * sinT), scl(b, sp * sinT)), scl(n, cosT)));
+}
+
+/* vndfRay (:382-435): direction */
+static v3 vndf_ray_dir(v3 V, v3 n, float roughness, float ux, float uy) {
+    const float alpha = roughness * roughness;
+    v3 T, B;
+    mis_onb(n, &T, &B);
+    const v3 Ve = nrm(mk(alpha * dot(V, T), alpha * dot(V, B), dot(V, n)));
+    const v3 T1 = nrm(mk(Ve.z, 0.0f, -Ve.x));
+    const v3 T2 = cross(Ve, T1);
+    const float phi = 2.0f * kPiF * ux;
+    const float lenVe = len(Ve);
+    const float ctm = lenVe / sqrtf(1.0f + lenVe * lenVe);
+    const float ct = ctm + (1.0f - ctm) * uy;
+    const float st = sqrtf(1.0f - ct * ct);
+    float sp, cp;
+    pto_sincos(phi, &sp, &cp);
+    const v3 h = nrm(add(add(scl(T1, cp * st), scl(T2, sp * st)), scl(Ve, ct)));
+    const v3 Nh = nrm(mk(alpha * h.x, alpha * h.y, fmaxf(0.0f, h.z)));
+    const v3 wH = nrm(add(add(scl(T, Nh.x), scl(B, Nh.y)), scl(n, Nh.z)));
+    const v3 I = neg(V);
+    return sub(I, scl(wH, 2.0f * dot(wH, I)));  /* reflect(I, wH) = I - 2*dot(wH,I)*wH */
+}
+
+/* calculateDirectLightSamplingContribution (:519-541) */
+static v3 direct_light(const scene_t* s, const mis_light* L, const mis_isect* x, float ux,
+                       float uy, uint32_t spp, int use_power) {
+    v3 direct = mk(0.0f, 0.0f, 0.0f);
+    /* directSquareLightRay(point + normal * 1e-4, light, u) (:291-313) */
+    const v3 origin = add(x->point, scl(x->normal, 1e-4f));
+    const float sx = (ux - 0.5f) * L->width;
+    const float sy = (uy - 0.5f) * L->depth;
+    const v3 sp = add(add(L->center, scl(L->tangent, sx)), scl(L->bitangent, sy));
+    const v3 toL = sub(sp, origin);
+    const float dist = len(toL);
+    const v3 ldir = divs(toL, dist);
+    const mis_isect li = closest_isect(s, origin, ldir, 0.001f, dist);
+    if (li.type == MIS_HIT_LIGHT) {
+        const float dl_pdf = light_pdf(L, x->point, ldir);
+        const v3 c = brdf(x->rd, x->normal, x->mat, ldir);
+        if (use_power) {
+            const float cos_pdf = cosine_pdf(x->normal, ldir);
+            const float v_pdf = vndf_pdf(neg(x->rd), x->normal, ldir, x->mat->roughness);
+            const float w = power_h(dl_pdf, cos_pdf, v_pdf, spp);
+            direct = add(direct, divs(mul(scl(c, w), L->radiance), dl_pdf));
+        } else {
+            direct = add(direct, divs(mul(c, L->radiance), dl_pdf));
+        }
+    }
+    return direct;
+}
+
+/* recursiveMultiImportanceSampling (:543-625) */
+static v3 mis_estimate(const scene_t* s, const mis_light* L, const mis_isect* x, uint32_t samples) {
+    const uint32_t S = samples / 3;
+    v3 dl = mk(0, 0, 0), cs = mk(0, 0, 0), vn = mk(0, 0, 0);
+    for (uint32_t i = 0; i < S; ++i)  /* :553-560, haltonRandom(i, 0) */
+        dl = add(dl, direct_light(s, L, x, pto_halton(i, 0), pto_halton(i, 1), S, 1));
+    const v3 origin = add(x->point, scl(x->normal, 1e-4f));
+    const v3 V = neg(x->rd);
+    for (uint32_t i = 0; i < S; ++i) {  /* :562-591 */
+        const v3 dir = cosine_ray_dir(x->normal, pto_halton(i + S, 2), pto_halton(i + S, 3));
+        const float cos_pdf = cosine_pdf(x->normal, dir);
+        const float dl_pdf = light_pdf(L, x->point, dir);
+        const float v_pdf = vndf_pdf(V, x->normal, dir, x->mat->roughness);
+        const float w = power_h(cos_pdf, dl_pdf, v_pdf, S);
+        const mis_isect y = closest_isect(s, origin, dir, 0.001f, 1000.0f);
+        const v3 c = brdf(x->rd, x->normal, x->mat, dir);
+        if (y.type == MIS_HIT_LIGHT) {
+            cs = add(cs, divs(mul(scl(c, w), L->radiance), cos_pdf));
+        } else if (y.type == MIS_HIT) {
+            const v3 nee = direct_light(s, L, &y, pto_halton(i, 6), pto_halton(i, 7), 1, 0);
+            cs = add(cs, mul(divs(c, cos_pdf), nee));
+        }
+    }
+    for (uint32_t i = 0; i < S; ++i) {  /* :593-623 */
+        const v3 dir = vndf_ray_dir(V, x->normal, x->mat->roughness, pto_halton(i + 2 * S, 4),
+                                    pto_halton(i + 2 * S, 5));
+        const float v_pdf = vndf_pdf(V, x->normal, dir, x->mat->roughness);
+        const float cos_pdf = cosine_pdf(x->normal, dir);
+        const float dl_pdf = light_pdf(L, x->point, dir);
+        const float w = power_h(v_pdf, dl_pdf, cos_pdf, S);
+        const mis_isect y = closest_isect(s, origin, dir, 0.001f, 1000.0f);
+        const v3 c = brdf(x->rd, x->normal, x->mat, dir);
+        if (y.type == MIS_HIT_LIGHT) {
+            vn = add(vn, divs(mul(scl(c, w), L->radiance), v_pdf));
+        } else if (y.type == MIS_HIT) {
+            const v3 nee = direct_light(s, L, &y, pto_halton(i + S, 6), pto_halton(i + S, 7), 1, 0);
+            vn = add(vn, mul(divs(c, v_pdf), nee));
+        }
+    }
+    return divs(add(add(dl, cs), vn), (float)S);
+}
+
+/* portable log / exp / pow of DESIGN.md §3.11 (cephes logf / expf) */
+static uint32_t fbits(float x) { uint32_t u; memcpy(&u, &x, 4); return u; }
+static float bitsf(uint32_t u) { float x; memcpy(&x, &u, 4); return x; }
+static float log_pt(float x) {
+    const uint32_t bx = fbits(x);
+    int e = (int)(bx >> 23) - 126;
+    float m = bitsf((bx & 0x007FFFFFu) | 0x3F000000u);
+    if (m < 0.707106781f) { e -= 1; m = m + m - 1.0f; } else { m = m - 1.0f; }
+    const float z = m * m;
+    float y = 7.0376836292e-2f;
+    y = fmaf(y, m, -1.1514610310e-1f);
+    y = fmaf(y, m, 1.1676998740e-1f);
+    y = fmaf(y, m, -1.2420140846e-1f);
+    y = fmaf(y, m, 1.4249322787e-1f);
+    y = fmaf(y, m, -1.6668057665e-1f);
+    y = fmaf(y, m, 2.0000714765e-1f);
+    y = fmaf(y, m, -2.4999993993e-1f);
+    y = fmaf(y, m, 3.3333331174e-1f);
+    y = (y * m) * z;
+    const float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(-0.5f, z, y);
+    return fmaf(fe, 0.693359375f, m + y);
+}
+static float exp_pt(float x) {
+    const float z = floorf(x * 1.44269504088896341f + 0.5f);
+    float r = fmaf(-z, 0.693359375f, x);
+    r = fmaf(-z, -2.12194440e-4f, r);
+    float p = 1.9875691500e-4f;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    const float y = fmaf(p, r * r, r) + 1.0f;
+    return y * bitsf((uint32_t)((int)z + 127) << 23);
+}
+float pto_pow(float x, float y) {
+    if (!(x > 7.88860905e-31f)) return 0.0f;
+    return exp_pt(y * log_pt(x));
+}
+
+typedef struct {
+    const scene_t* s;
+    mis_light L;
+    uint32_t camera_rays, samples, row_start, row_step, row_count;
+    float exposure;
+    float* out;
+    uint8_t* out8;
+    uint32_t next_row;
+    pthread_mutex_t mu;
+} mis_job_t;
+
+static void mis_row(mis_job_t* J, uint32_t j) {
+    const scene_t* s = J->s;
+    const int32_t W = s->cam.W;
+    const uint32_t y = J->row_start + j * J->row_step;
+    for (int32_t xi = 0; xi < W; ++xi) {
+        const uint32_t x = (uint32_t)xi;
+        v3 acc = mk(0.0f, 0.0f, 0.0f);                       /* :645 */
+        for (uint32_t i = 0; i < J->camera_rays; ++i) {      /* :652 */
+            const uint32_t sample_id = (y * 800u + x) * i;   /* hashRandom :73 */
+            const float jx = random_float(x + y * 800u + sample_id);            /* :77,81 */
+            const float jy = random_float(y + x * 600u + sample_id + 12345u);   /* :78,82 */
+            const v3 d = cam_dir(&s->cam, (int32_t)x, (int32_t)y, jx, jy);     /* :214-246 */
+            const mis_isect h = closest_isect(s, s->cam.pos, d, 0.001f, 1000.0f); /* :660 */
+            if (h.type == MIS_MISS) {
+            } else if (h.type == MIS_HIT_LIGHT) {
+                acc = add(acc, J->L.radiance);                 /* :669-670 */
+            } else {
+                acc = add(acc, mis_estimate(s, &J->L, &h, J->samples)); /* :674-676 */
+            }
+        }
+        const size_t o = (size_t)j * (size_t)W + (size_t)xi;
+        const float nc = (float)J->camera_rays;
+        if (J->out) {  /* textBuffer (:705) + the divisor */
+            J->out[4 * o] = acc.x; J->out[4 * o + 1] = acc.y;
+            J->out[4 * o + 2] = acc.z; J->out[4 * o + 3] = nc;
+        }
+        if (J->out8) {  /* :688-706 */
+            const float e[3] = {acc.x / nc * J->exposure, acc.y / nc * J->exposure,
+                                acc.z / nc * J->exposure};
+            for (int k = 0; k < 3; ++k) {
+                const float tm = c01(e[k] / (e[k] + 1.0f));
+                const float g = pto_pow(tm, 1.0f / 2.2f);
+                J->out8[4 * o + k] = (uint8_t)(g * 255.0f);
+            }
+            J->out8[4 * o + 3] = 255;
+        }
+    }
+}
+
+static void* mis_worker(void* arg) {
+    mis_job_t* J = (mis_job_t*)arg;
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        const uint32_t j = J->next_row++;
+        pthread_mutex_unlock(&J->mu);
+        if (j >= J->row_count) break;
+        mis_row(J, j);
+    }
+    return NULL;
+}
+
+int pto_render_mis(const CameraGPU* cam, const MaterialGPU* mats, const SquareLightGPU* light,
+                   const rt_float3* verts, uint32_t n_tri, uint32_t camera_rays,
+                   uint32_t mis_samples, uint32_t row_start, uint32_t row_step,
+                   uint32_t row_count, float* out, uint8_t* out8, int nthreads) {
+    if (!cam || !light || !mats || !verts || n_tri == 0 || camera_rays == 0 || mis_samples < 3)
+        return -1;
+    if (cam->resolution.x <= 0 || cam->resolution.y <= 0) return -1;
+    if (row_step == 0) row_step = 1;
+    if (row_start >= (uint32_t)cam->resolution.y) return -1;
+    if (row_count == 0) row_count = ((uint32_t)cam->resolution.y - 1u - row_start) / row_step + 1u;
+    if ((uint64_t)row_start + (uint64_t)(row_count - 1) * row_step >= (uint64_t)cam->resolution.y)
+        return -1;
+    scene_t s;
+    if (scene_build(&s, cam, mats, light, verts, n_tri, NULL, 0)) return -1;
+    mis_job_t J;
+    memset(&J, 0, sizeof(J));
+    J.s = &s;
+    J.L.center = ld3(&light->center);
+    mis_onb(mk(0.0f, -1.0f, 0.0f), &J.L.tangent, &J.L.bitangent);  /* :292-293 */
+    J.L.radiance = ld3(&light->emittedRadiance);
+    J.L.width = light->width;
+    J.L.depth = light->depth;
+    {
+        volatile float ev = cam->ev100;                        /* cameraExposure :145-150 */
+        J.exposure = 1.0f / (1.2f * powf(2.0f, ev));
+    }
+    J.camera_rays = camera_rays;
+    J.samples = mis_samples;
+    J.row_start = row_start;
+    J.row_step = row_step;
+    J.row_count = row_count;
+    J.out = out;
+    J.out8 = out8;
+    pthread_mutex_init(&J.mu, NULL);
+    if (nthreads <= 1) {
+        mis_worker(&J);
+    } else {
+        pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+        int started = 0;
+        for (int k = 0; k < nthreads; ++k)
+            if (pthread_create(&th[k], NULL, mis_worker, &J) == 0) ++started;
+        if (started == 0) mis_worker(&J);
+        for (int k = 0; k < started; ++k) pthread_join(th[k], NULL);
+        free(th);
+    }
+    pthread_mutex_destroy(&J.mu);
+    scene_free(&s);
+    return 0;
 }

@@ -75,6 +75,19 @@ int pto_random_spheres(int32_t width, int32_t height, uint32_t n_spheres, uint64
                        SquareLightGPU* light, uint32_t* n_tri, SphereGPU* spheres);
 void pto_seed_splitmix(uint64_t key, uint32_t* seeds, size_t n);
 
+/* MIS integrator (Sources/gpuRaytracer/shaders.metal:635-707): rows as in
+ * pto_render; out (optional) = (sum over camera rays, camera_rays) float4,
+ * out8 (optional) = the tonemapped RGBA8 of :688-706. */
+int pto_render_mis(const CameraGPU* cam, const MaterialGPU* mats, const SquareLightGPU* light,
+                   const rt_float3* verts, uint32_t n_tri, uint32_t camera_rays,
+                   uint32_t mis_samples, uint32_t row_start, uint32_t row_step,
+                   uint32_t row_count, float* out, uint8_t* out8, int nthreads);
+/* Sources/gpuRaytracer/main.swift:21-67 scene (1.5 x 1.5 light) */
+int pto_cornell_box_mis(int32_t width, int32_t height, CameraGPU* cam, MaterialGPU* mats,
+                        rt_float3* verts, SquareLightGPU* light, uint32_t* n_tri);
+/* pow(x, y), x in [0, 1], of the DESIGN.md §3.11 contract */
+float pto_pow(float x, float y);
+
 /* image.swift:35-65 epilogue */
 void pto_tonemap_rgba8(const float* rgba32f, size_t n_pixels, uint8_t* rgba8);
 

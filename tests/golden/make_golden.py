@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import oracle_lib  # noqa: E402
+import pt_oracle_mis_np  # noqa: E402
 import pt_oracle_np  # noqa: E402
 from gpuraytracer_amd import Scene  # noqa: E402
 
@@ -53,6 +54,19 @@ def make(name, scene, seeds, spp, bounces, sample_base=0):
         raise SystemExit(f"{name}: C oracle != numpy restatement at {bad[:5].tolist()}")
     np.savez_compressed(os.path.join(HERE, name + ".npz"), seeds=seeds, out=out,
                         params=np.array([spp, bounces, sample_base], np.uint32),
+                        **scene_bytes(scene))
+    print(f"{name}: {out.shape} mean {out[..., :3].mean():.6f} (C == numpy, bit-exact)")
+
+
+def make_mis(name, scene, camera_rays, mis_samples):
+    """MIS integrator fixture: C oracle checked against pt_oracle_mis_np first."""
+    out, out8 = oracle_lib.render_mis(scene, camera_rays, mis_samples)
+    sc = pt_oracle_mis_np.Scene(scene.camera, scene.materials, scene.light, scene.vertices)
+    ref, ref8 = pt_oracle_mis_np.render_mis(sc, camera_rays, mis_samples)
+    if not (np.array_equal(out.view(np.uint32), ref.view(np.uint32)) and np.array_equal(out8, ref8)):
+        raise SystemExit(f"{name}: C oracle != numpy MIS restatement")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), out=out, out8=out8,
+                        params=np.array([camera_rays, mis_samples], np.uint32),
                         **scene_bytes(scene))
     print(f"{name}: {out.shape} mean {out[..., :3].mean():.6f} (C == numpy, bit-exact)")
 
@@ -136,6 +150,7 @@ def main():
     make("cornell_24x13_s3_b4_u32seeds", s, sd, 3, 4, sample_base=5)
     s = Scene.random_spheres(16, 16, 60, seed=42)
     make("spheres60_16x16_s2_b3", s, oracle_lib.seeds(16, 16, key), 2, 3)
+    make_mis("mis_16x12_c2_m12", Scene.cornell_box_mis(16, 12), 2, 12)
     footprint_from_png()
 
 

@@ -77,3 +77,32 @@ def tonemap(rgba32f):
     _lib.pto_tonemap_rgba8(a.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(a.size // 4),
                            out.ctypes.data_as(ctypes.c_void_p))
     return out
+
+
+_lib.pto_pow.restype = ctypes.c_float
+_lib.pto_pow.argtypes = [ctypes.c_float, ctypes.c_float]
+_lib.pto_render_mis.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] * 6 + \
+    [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+
+
+def cornell_box_mis(width, height):
+    cam, light = CameraGPU(), SquareLightGPU()
+    mats, verts, n = (MaterialGPU * 36)(), (float3 * 108)(), ctypes.c_uint32()
+    assert _lib.pto_cornell_box_mis(width, height, ctypes.byref(cam), mats, verts,
+                                    ctypes.byref(light), ctypes.byref(n)) == 0
+    return cam, mats, verts, light, n.value
+
+
+def render_mis(scene, camera_rays=6, mis_samples=300, row_start=0, row_step=1, row_count=0,
+               threads=None):
+    """Oracle MIS render (pto_render_mis); returns (sum float32, rgba8)."""
+    H, W = scene.height, scene.width
+    rows = row_count or (H - 1 - row_start) // row_step + 1
+    out = np.zeros((rows, W, 4), np.float32)
+    out8 = np.zeros((rows, W, 4), np.uint8)
+    threads = threads or min(8, os.cpu_count() or 1)
+    r = _lib.pto_render_mis(_p(scene.camera), _p(scene.materials), _p(scene.light),
+                            _p(scene.vertices), scene.n_triangles, camera_rays, mis_samples,
+                            row_start, row_step, row_count, _p(out), _p(out8), threads)
+    assert r == 0, "oracle rejected the input"
+    return out, out8

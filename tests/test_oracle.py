@@ -273,3 +273,84 @@ def test_halton_small_magic_table():
     for b, m, s in zip(primes, M, S):
         assert m < (1 << 24) and s < 32
         assert np.array_equal((i * np.uint64(m)) >> np.uint64(s), i // np.uint64(b)), b
+
+
+# ---- MIS integrator (Sources/gpuRaytracer/shaders.metal) ----------------------------
+def test_mis_scene_builder_equals_oracle_and_main_swift():
+    s = Scene.cornell_box_mis(800, 600)
+    cam, mats, verts, light, n = oracle_lib.cornell_box_mis(800, 600)
+    assert n == 36
+    for a, b in ((s.camera, cam), (s.materials, mats), (s.vertices, verts), (s.light, light)):
+        assert bytes(a) == bytes(b)
+    # main.swift:27-28,49-59: 1.5 x 1.5 light; emittedLuminance = diffuse * 1200 / 2.25 / Float.pi
+    assert light.width == 1.5 and light.depth == 1.5
+    lum = np.float32(np.float32(1200.0) / np.float32(2.25)) / np.float32(3.1415925)
+    assert light.emittedRadiance.x == np.float32(1.0) * lum
+    assert light.emittedRadiance.y == np.float32(0.95) * lum
+    v = np.frombuffer(bytes(verts), np.float32).reshape(-1, 4)
+    assert np.array_equal(v[102:108, [0, 2]].min(0), [-0.75, -0.75])
+    # the room and boxes are RTrace's
+    assert np.array_equal(v[:102], np.frombuffer(bytes(Scene.cornell_box(800, 600).vertices),
+                                                 np.float32).reshape(-1, 4)[:102])
+
+
+def test_pow_contract_accuracy():
+    xs = np.concatenate([np.geomspace(1e-30, 1.0, 4000, dtype=np.float32),
+                         np.linspace(0, 1, 4001, dtype=np.float32)])
+    y = np.float32(1.0) / np.float32(2.2)
+    got = np.array([oracle_lib.lib.pto_pow(float(x), float(y)) for x in xs], np.float32)
+    ref = np.power(xs.astype(np.float64), float(y))
+    ok = xs > 7.88860905e-31
+    rel = np.abs(got[ok] - ref[ok]) / ref[ok]
+    # exp(y log x): error ~ |y log x| * 2^-24, i.e. a few ulp where a byte of
+    # gamma output is decided (x >= 1e-3) and < 4e-6 relative down to 1e-30
+    assert rel.max() < 4e-6, rel.max()
+    assert rel[xs[ok] >= 1e-3].max() < 6e-7
+    assert np.all(got[~ok] == 0) and oracle_lib.lib.pto_pow(1.0, float(y)) == 1.0
+    import pt_oracle_mis_np as M
+    assert np.array_equal(M.pow_pt(xs, y).view(np.uint32), got.view(np.uint32))
+
+
+@pytest.mark.parametrize("w,h,rays,samples", [(8, 6, 2, 6), (7, 5, 1, 9)])
+def test_mis_oracle_equals_numpy_restatement(w, h, rays, samples):
+    import pt_oracle_mis_np as M
+    s = Scene.cornell_box_mis(w, h)
+    out, out8 = oracle_lib.render_mis(s, rays, samples)
+    sc = M.Scene(s.camera, s.materials, s.light, s.vertices)
+    ref, ref8 = M.render_mis(sc, rays, samples)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(out8, ref8)
+
+
+def test_mis_oracle_reproduces_golden():
+    from gpuraytracer_amd import CameraGPU, MaterialGPU, SquareLightGPU, float3
+    g = np.load(os.path.join(GOLDEN, "mis_16x12_c2_m12.npz"))
+    s = Scene(CameraGPU.from_buffer_copy(g["camera"].tobytes()),
+              (MaterialGPU * 36).from_buffer_copy(g["materials"].tobytes()),
+              (float3 * 108).from_buffer_copy(g["vertices"].tobytes()),
+              SquareLightGPU.from_buffer_copy(g["light"].tobytes()))
+    rays, samples = (int(v) for v in g["params"])
+    out, out8 = oracle_lib.render_mis(s, rays, samples)
+    assert np.array_equal(out.view(np.uint32), g["out"].view(np.uint32))
+    assert np.array_equal(out8, g["out8"])
+
+
+def test_mis_light_pixels_known_answer():
+    # a pixel whose camera rays all hit the light sums emittedRadiance camera_rays
+    # times (shaders.metal:667-671) and tonemaps to a fixed byte (:688-706)
+    s = Scene.cornell_box_mis(80, 60)
+    out, out8 = oracle_lib.render_mis(s, 6, 3, row_start=8, row_count=6)
+    Le = np.array([s.light.emittedRadiance.x, s.light.emittedRadiance.y,
+                   s.light.emittedRadiance.z], np.float32)
+    six = np.zeros(3, np.float32)
+    for _ in range(6):
+        six = six + Le
+    lit = np.all(out[..., :3] == six, axis=-1)
+    ys, xs = np.nonzero(lit)
+    assert lit.sum() >= 8 and 30 <= xs.min() and xs.max() <= 49  # centred light patch
+    import pt_oracle_mis_np as M
+    e = (six / np.float32(6)) * (np.float32(1) / (np.float32(1.2) * np.float32(32.0)))
+    tm = np.minimum(np.float32(1), np.maximum(np.float32(0), e / (e + np.float32(1))))
+    expect = (M.pow_pt(tm, np.float32(1) / np.float32(2.2)) * np.float32(255)).astype(np.uint8)
+    assert np.all(out8[lit][:, :3] == expect) and np.all(out8[..., 3] == 255)
+    assert np.all(out[..., 3] == 6)
