@@ -195,7 +195,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.nT = (uint32_t)c->scene.tri_isect.size();
     K.nS = (uint32_t)c->scene.sph_isect.size();
     K.nP = (uint32_t)c->scene.pair_isect.size();
-    K.nN = (uint32_t)c->scene.sph_nodes.size();
+    K.nN = c->scene.sph_layout_nodes;
     const rt::CamConst& cam = c->scene.cam;
     memcpy(K.cam_pos, cam.pos, sizeof(K.cam_pos));
     memcpy(K.cam_u, cam.u, sizeof(K.cam_u));
@@ -433,6 +433,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
         if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
         if (!strcmp(m, "sorted")) c->scene_mem = rt::SceneMem::kPairSorted;
+        if (!strcmp(m, "pairsmem")) c->scene_mem = rt::SceneMem::kPairSmem;
     }
     DeviceGuard g(c->device);
     const char* err = nullptr;
@@ -545,9 +546,9 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     info->n_triangles = (uint32_t)s.tri_isect.size();
     info->n_triangle_pairs = (uint32_t)s.pair_isect.size();
     info->n_spheres = (uint32_t)s.sph_isect.size();
-    info->n_sphere_nodes = (uint32_t)s.sph_nodes.size();
+    info->n_sphere_nodes = s.sph_layout_nodes;
     const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres,
-                                            (uint32_t)s.sph_nodes.size());
+                                            s.sph_layout_nodes);
     info->lds_bytes = lds <= rt::kMaxLdsBytes ? (uint32_t)lds : 0u;
     return RT_OK;
 }

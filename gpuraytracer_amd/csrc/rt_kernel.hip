@@ -219,7 +219,7 @@ constexpr uint32_t kSortLum = kSortD + kBlockThreads / 2;  // float sum x[256], 
 constexpr uint32_t kSortCnt = kSortLum + 3 * kBlockThreads / 4;  // uint [bucket][wave]
 constexpr uint32_t kSortF4 = kSortCnt + (kSortBuckets * 4 + 3) / 4;
 
-__device__ __forceinline__ uint32_t octant(f3 d) {
+__device__ __forceinline__ uint32_t sort_octant(f3 d) {
     return (d.x > 0.0f ? 4u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 1u : 0u);
 }
 
@@ -233,7 +233,7 @@ __device__ __forceinline__ void sort_paths(float4* lds, PathState& s, uint32_t& 
                                            bool& alive) {
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     uint32_t* counts = reinterpret_cast<uint32_t*>(lds + kSortCnt);
-    const uint32_t key = alive ? octant(s.d) : 8u;
+    const uint32_t key = alive ? sort_octant(s.d) : 8u;
     uint32_t my_count = 0, slot = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kSortBuckets - 1; ++k) {
@@ -334,7 +334,10 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
     sv.nT = P.nT;
     sv.nP = P.nP;
     sv.nS = SPH ? P.nS : 0u;
-    if (GEO != kGeoTriGlobal) {
+    if (GEO == kGeoPairSmem) {
+        sv.tri = nullptr;
+        sv.pair = P.pair_isect;
+    } else if (GEO != kGeoTriGlobal) {
         // Stage the intersection records once per workgroup.
         const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
@@ -488,7 +491,7 @@ template <int B, int GEO, bool SPH, bool SMALL>
 hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(kBlockThreads),
-                       GEO == kGeoTriGlobal ? 0 : lds_bytes, stream, P);
+                       (GEO == kGeoTriGlobal || GEO == kGeoPairSmem) ? 0 : lds_bytes, stream, P);
     return hipGetLastError();
 }
 
@@ -525,6 +528,7 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
     }
     switch (geo) {
         case kGeoPairLds: return launch_g<B, kGeoPairLds>(P, lds_bytes, stream);
+        case kGeoPairSmem: return launch_g<B, kGeoPairSmem>(P, lds_bytes, stream);
         case kGeoTriLds: return launch_g<B, kGeoTriLds>(P, lds_bytes, stream);
         default: return launch_g<B, kGeoTriGlobal>(P, lds_bytes, stream);
     }
@@ -545,6 +549,7 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
     const size_t lds_bytes = kernel_lds_bytes(P.nT, pairs ? P.nP : 0u, P.nS, P.nN);
     int geo = kGeoTriGlobal;
     if (mem != SceneMem::kSmem && lds_bytes <= kMaxLdsBytes) geo = pairs ? kGeoPairLds : kGeoTriLds;
+    if (mem == SceneMem::kPairSmem && P.nP > 0) geo = kGeoPairSmem;
     // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the
     // Cornell 1080p workload (barrier + occupancy cost).
     if (geo == kGeoPairLds && mem == SceneMem::kPairSorted &&

@@ -42,7 +42,7 @@ struct KParams {
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);
 // Where the workgroup reads the intersection records from.
-enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3 };
+enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
 hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
 // Arguments of the MIS integrator kernel (rt_mis.hip; Sources/gpuRaytracer/

@@ -256,16 +256,25 @@ static float culling_margin(const rt_float3* verts, uint32_t n_tri, const Sphere
     return 4e-5f * ext;
 }
 
-// Depth-first BVH over the spheres (median split of the centroids on the
-// longest axis, <= 4 spheres per leaf).  Only speed depends on its shape: the
-// kernel's traversal skips a node only when no sphere inside can beat the
-// current closest hit, and ties are resolved by sphere id, so the result is
-// that of testing every sphere in id order.
+// BVH over the spheres (median split of the centroids on the longest axis,
+// <= 4 spheres per leaf), emitted as 8 depth-first layouts, one per ray-direction
+// octant: at every inner node the child on the near side of the split for that
+// octant comes first, so a closest-hit walk meets near spheres early and culls
+// more.  Only speed depends on the tree and the order: the kernel skips a node
+// only when no sphere inside can beat the current closest hit, and ties are
+// resolved by sphere id, so the result is that of testing every sphere in id
+// order.
 struct BvhBuild {
+    struct Node {
+        float lo[3], hi[3];
+        int axis;                 // split axis (inner nodes)
+        uint32_t left, right;     // children (inner nodes)
+        uint32_t first, count;    // sphere range (leaves), count 0 for inner nodes
+    };
     const SphereGPU* sph;
     float margin;
     std::vector<uint32_t> ids;
-    std::vector<BvhNode> nodes;
+    std::vector<Node> tree;
 
     void bounds(uint32_t b, uint32_t e, float lo[3], float hi[3], bool centroids) const {
         for (int a = 0; a < 3; ++a) {
@@ -283,35 +292,59 @@ struct BvhBuild {
         }
     }
 
-    void build(uint32_t b, uint32_t e) {
-        const uint32_t me = (uint32_t)nodes.size();
-        nodes.push_back(BvhNode{});
+    uint32_t build(uint32_t b, uint32_t e) {
+        const uint32_t me = (uint32_t)tree.size();
+        tree.push_back(Node{});
         float lo[3], hi[3];
         bounds(b, e, lo, hi, false);
         for (int a = 0; a < 3; ++a) {
-            nodes[me].lo[a] = lo[a] - margin;
-            nodes[me].hi[a] = hi[a] + margin;
+            tree[me].lo[a] = lo[a] - margin;
+            tree[me].hi[a] = hi[a] + margin;
         }
         if (e - b <= 4) {
-            nodes[me].leaf = ((e - b) << 24) | b;
-        } else {
-            float clo[3], chi[3];
-            bounds(b, e, clo, chi, true);
-            int axis = 0;
-            for (int a = 1; a < 3; ++a)
-                if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
-            const uint32_t mid = b + (e - b) / 2;
-            std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
-                             [&](uint32_t x, uint32_t y) {
-                                 const float cx[3] = {sph[x].center.x, sph[x].center.y, sph[x].center.z};
-                                 const float cy[3] = {sph[y].center.x, sph[y].center.y, sph[y].center.z};
-                                 return cx[axis] < cy[axis] || (cx[axis] == cy[axis] && x < y);
-                             });
-            nodes[me].leaf = 0;
-            build(b, mid);
-            build(mid, e);
+            tree[me].first = b;
+            tree[me].count = e - b;
+            return me;
         }
-        nodes[me].escape = (uint32_t)nodes.size();
+        float clo[3], chi[3];
+        bounds(b, e, clo, chi, true);
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+        const uint32_t mid = b + (e - b) / 2;
+        std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
+                         [&](uint32_t x, uint32_t y) {
+                             const float cx[3] = {sph[x].center.x, sph[x].center.y, sph[x].center.z};
+                             const float cy[3] = {sph[y].center.x, sph[y].center.y, sph[y].center.z};
+                             return cx[axis] < cy[axis] || (cx[axis] == cy[axis] && x < y);
+                         });
+        const uint32_t l = build(b, mid);
+        const uint32_t r = build(mid, e);
+        tree[me].axis = axis;
+        tree[me].left = l;
+        tree[me].right = r;
+        tree[me].count = 0;
+        return me;
+    }
+
+    // Depth-first emission for octant `oct` (bit a set: direction component a < 0).
+    void emit(uint32_t t, int oct, std::vector<BvhNode>* out) const {
+        const Node& n = tree[t];
+        const uint32_t me = (uint32_t)out->size();
+        out->push_back(BvhNode{});
+        for (int a = 0; a < 3; ++a) {
+            (*out)[me].lo[a] = n.lo[a];
+            (*out)[me].hi[a] = n.hi[a];
+        }
+        if (n.count) {
+            (*out)[me].leaf = (n.count << 24) | n.first;
+        } else {
+            const bool neg = (oct >> n.axis) & 1;  // moving toward lower coordinates
+            emit(neg ? n.right : n.left, oct, out);
+            emit(neg ? n.left : n.right, oct, out);
+            (*out)[me].leaf = 0;
+        }
+        (*out)[me].escape = (uint32_t)out->size();
     }
 };
 
@@ -320,6 +353,7 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
     out->sph_isect.clear();
     out->sph_perm.clear();
     out->sph_nodes.clear();
+    out->sph_layout_nodes = 0;
     if (n == 0) return;
     BvhBuild bb;
     bb.sph = spheres;
@@ -327,7 +361,14 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
     bb.ids.resize(n);
     for (uint32_t k = 0; k < n; ++k) bb.ids[k] = k;
     bb.build(0, n);
-    out->sph_nodes.swap(bb.nodes);
+    const uint32_t nn = (uint32_t)bb.tree.size();
+    for (int oct = 0; oct < 8; ++oct) {
+        std::vector<BvhNode> layout;
+        layout.reserve(nn);
+        bb.emit(0, oct, &layout);
+        out->sph_nodes.insert(out->sph_nodes.end(), layout.begin(), layout.end());
+    }
+    out->sph_layout_nodes = nn;
     out->sph_perm = bb.ids;
     out->sph_isect.resize(n);
     for (uint32_t k = 0; k < n; ++k) {

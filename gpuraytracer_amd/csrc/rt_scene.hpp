@@ -45,7 +45,8 @@ struct SphIsect {
 // traversal): n0 = (lo.xyz, escape), n1 = (hi.xyz, leaf); escape = index of
 // the node after this subtree; leaf = count << 24 | first (count 0: internal
 // node whose first child is the next node).  Boxes are padded by the culling
-// margin.
+// margin.  Eight layouts (one per ray-direction octant,
+// near child first) of the same tree are stored back to back.
 struct BvhNode {
     float lo[3];
     uint32_t escape;
@@ -93,7 +94,8 @@ struct CompiledScene {
     std::vector<PairIsect> pair_isect;  // empty unless every (2k, 2k+1) shares v0 + an edge
     std::vector<SphIsect> sph_isect;    // in BVH leaf order
     std::vector<uint32_t> sph_perm;     // leaf-order index -> sphere id (shading, ties)
-    std::vector<BvhNode> sph_nodes;
+    std::vector<BvhNode> sph_nodes;     // 8 octant layouts of sph_layout_nodes nodes each
+    uint32_t sph_layout_nodes = 0;
     std::vector<SphShade> sph_shade;    // by sphere id
     MisLightConst mis_light;
     std::vector<MisShade> mis_shade;    // by triangle id

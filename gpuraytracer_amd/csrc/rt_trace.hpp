@@ -132,8 +132,11 @@ __device__ __forceinline__ void stat_wave(int slot, unsigned long long v) {
 enum Geo : int {
     kGeoTriLds = 0,     // single-triangle records staged in LDS
     kGeoPairLds = 1,    // shared-edge pair records staged in LDS
+    kGeoPairSmem = 4,   // shared-edge pair records read with scalar loads (no LDS)
     kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
 };
+
+constexpr bool geo_pairs(int g) { return g == kGeoPairLds || g == kGeoPairSmem; }
 
 struct SceneView {
     const float4* tri;        // 3 float4 per triangle (single layout)
@@ -177,6 +180,12 @@ __device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, con
 #define RT_SPH_PACKET 1  // 1: packet walks for camera and bounce-0 shadow rays; 2: + all shadow rays; 3: all
 #endif
 
+// BVH layout of a ray direction: bit a set when component a is negative.
+__device__ __forceinline__ uint32_t octant(f3 d) {
+    return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
+           ((__float_as_uint(d.z) >> 31) << 2);
+}
+
 __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
@@ -198,6 +207,7 @@ __device__ __forceinline__ void sphere_closest(const float4* __restrict__ node,
     // id-ordered scan with strict '<', so the visiting order is free.
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
+    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
     uint32_t idx = 0;
     while (idx < nN) {
         const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
@@ -231,6 +241,7 @@ __device__ __forceinline__ bool sphere_any(const float4* __restrict__ node,
                                            f3 d, float tmin, float tmax) {
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
+    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
     bool found = false;
     uint32_t idx = 0;
     while (idx < nN) {
@@ -282,7 +293,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
                                            float* t_io) {
     float best = *t_io;
     int id = -1;
-    if (GEO == kGeoPairLds) {
+    if (geo_pairs(GEO)) {
         f3 seg_lo, seg_hi;
         if (CULL) {
             const f3 e = o + d * best;
@@ -351,7 +362,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
 template <int GEO, bool SPH, bool PACKET>
 __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
                                         f3 seg_lo, f3 seg_hi) {
-    if (GEO == kGeoPairLds) {
+    if (geo_pairs(GEO)) {
         for (uint32_t k = 0; k < sv.nP; ++k) {
             const float4* r = sv.pair + kPairF4 * k;
             const float4 b0 = r[5], b1 = r[6];

@@ -160,7 +160,7 @@ def test_errors_are_status_codes():
         assert out.shape == (8, 16, 4)
 
 
-@pytest.mark.parametrize("layout", ["single", "smem", "sorted"])
+@pytest.mark.parametrize("layout", ["single", "smem", "sorted", "pairsmem"])
 def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
     """The single-triangle LDS layout, the global (scalar-load) layout and the
     octant-sorted path kernel give the same bits as the default pair kernel
