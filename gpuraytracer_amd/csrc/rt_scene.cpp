@@ -2,6 +2,7 @@
 // Compiled with -ffp-contract=off (see rt_math.h).
 #include "rt_scene.hpp"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -257,7 +258,7 @@ static float culling_margin(const rt_float3* verts, uint32_t n_tri, const Sphere
 }
 
 // BVH over the spheres (median split of the centroids on the longest axis,
-// <= 4 spheres per leaf), emitted as 8 depth-first layouts, one per ray-direction
+// one sphere per leaf by default), emitted as 8 depth-first layouts, one per ray-direction
 // octant: at every inner node the child on the near side of the split for that
 // octant comes first, so a closest-hit walk meets near spheres early and culls
 // more.  Only speed depends on the tree and the order: the kernel skips a node
@@ -273,6 +274,7 @@ struct BvhBuild {
     };
     const SphereGPU* sph;
     float margin;
+    uint32_t leaf_max = 1;  // measured best for config 4 (RTPT_BVH_LEAF sweep 1..8)
     std::vector<uint32_t> ids;
     std::vector<Node> tree;
 
@@ -301,7 +303,7 @@ struct BvhBuild {
             tree[me].lo[a] = lo[a] - margin;
             tree[me].hi[a] = hi[a] + margin;
         }
-        if (e - b <= 4) {
+        if (e - b <= leaf_max) {
             tree[me].first = b;
             tree[me].count = e - b;
             return me;
@@ -358,6 +360,10 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
     BvhBuild bb;
     bb.sph = spheres;
     bb.margin = margin;
+    if (const char* lm = getenv("RTPT_BVH_LEAF")) {  // tuning knob (speed only)
+        const int v = atoi(lm);
+        if (v >= 1 && v <= 255) bb.leaf_max = (uint32_t)v;
+    }
     bb.ids.resize(n);
     for (uint32_t k = 0; k < n; ++k) bb.ids[k] = k;
     bb.build(0, n);

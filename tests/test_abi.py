@@ -79,8 +79,8 @@ def test_scene_layout_uses_shared_edge_pairs():
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
                     "lds_bytes": 18 * 112, "n_sphere_nodes": 0}
 
-    def bvh_nodes(n):  # median split, <= 4 spheres per leaf (rt_scene.cpp BvhBuild)
-        return 1 if n <= 4 else 1 + bvh_nodes(n // 2) + bvh_nodes(n - n // 2)
+    def bvh_nodes(n):  # median split, one sphere per leaf (rt_scene.cpp BvhBuild)
+        return 1 if n <= 1 else 1 + bvh_nodes(n // 2) + bvh_nodes(n - n // 2)
 
     info = g.Scene.random_spheres(64, 48, 1000).describe()
     assert info["n_sphere_nodes"] == bvh_nodes(1000)

@@ -1,3 +1,2 @@
 set -e
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q > gpurun_out/tests.log 2>&1
-timeout -k 10 200 python bench.py --scene spheres --steps 3 --warmup 1 --cpu-baseline off > gpurun_out/sph_oct.log 2>&1
+for l in 1 2 3 4 6 8; do RTPT_BVH_LEAF=$l timeout -k 10 200 python bench.py --scene spheres --steps 3 --warmup 1 --cpu-baseline off > gpurun_out/sph_leaf$l.log 2>&1; done
