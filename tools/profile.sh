@@ -13,7 +13,15 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=(python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline off "$@")
+# PROFILE_TARGET=mis profiles the MIS integrator (tools/bench_mis.py) instead.
+if [ "${PROFILE_TARGET:-pathtrace}" = mis ]; then
+  BENCH=(python3 "$R/tools/bench_mis.py" --steps 3 --warmup 1 --cpu-seconds 0 "$@")
+  KRE=mis_kernel
+else
+  BENCH=(python3 "$R/bench.py" --steps 3 --warmup 1 --cpu-baseline off "$@")
+  KRE=path_trace
+fi
+export PROFILE_KERNEL=$KRE
 
 run() {  # run <name> <rocprof args...>
   local name=$1; shift
@@ -31,11 +39,11 @@ run() {  # run <name> <rocprof args...>
 
 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1 || true
 run trace --kernel-trace --stats
-run fetch --pmc FETCH_SIZE --kernel-include-regex path_trace
-run write --pmc WRITE_SIZE --kernel-include-regex path_trace
-run sq_insts --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_BRANCH --kernel-include-regex path_trace
-run sq_cycles --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-include-regex path_trace
-run sq_valu --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT --kernel-include-regex path_trace
-run sq_lds --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_WAIT_INST_LDS --kernel-include-regex path_trace
+run fetch --pmc FETCH_SIZE --kernel-include-regex $KRE
+run write --pmc WRITE_SIZE --kernel-include-regex $KRE
+run sq_insts --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_BRANCH --kernel-include-regex $KRE
+run sq_cycles --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-include-regex $KRE
+run sq_valu --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT --kernel-include-regex $KRE
+run sq_lds --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_WAIT_INST_LDS --kernel-include-regex $KRE
 python3 "$R/tools/summarize_profile.py" "$OUT" "${BENCH[@]:1}" > "$OUT/summary.json"
 cat "$OUT/summary.json"

@@ -16,10 +16,18 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "path_trace"
+KERNEL = os.environ.get("PROFILE_KERNEL", "path_trace")
 
 
 def bench_workload(argv):
+    if argv and argv[0].endswith("bench_mis.py"):
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--width", type=int, default=800)
+        ap.add_argument("--height", type=int, default=600)
+        ap.add_argument("--camera-rays", type=int, default=6)
+        ap.add_argument("--mis-samples", type=int, default=300)
+        a, _ = ap.parse_known_args(argv[1:])
+        return f"mis_{a.width}x{a.height}_c{a.camera_rays}_m{a.mis_samples}"
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--width", type=int, default=1920)
