@@ -1,2 +1,3 @@
 set -e
-for v in w4 w5 w6 w7; do RTPT_LIB=variants/librtpt_$v.so timeout -k 10 200 python bench.py --scene spheres --steps 3 --warmup 1 --cpu-baseline off > gpurun_out/sph_$v.log 2>&1; done
+timeout -k 10 600 python -m pytest tests/test_gpu_mis.py -x -q > gpurun_out/tests.log 2>&1
+timeout -k 10 300 python tools/bench_mis.py > gpurun_out/mis.log 2>&1
