@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=256, help="samples per pixel per GPU")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--spheres", type=int, default=1000)
+    ap.add_argument("--batch-spp", type=int, default=0,
+                    help="progressive mode: launches of this many spp into a running sum")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
@@ -136,6 +138,8 @@ def main():
     if args.scene == "cornell":
         scene = Scene.cornell_box(W, H)
         workload = f"cornell_{W}x{H}_{args.spp}spp_b{args.bounces}"
+        if args.batch_spp:
+            workload += f"_progressive{args.batch_spp}"
     else:
         scene = Scene.random_spheres(W, H, args.spheres, seed=42)
         workload = f"spheres{args.spheres}_{W}x{H}_{args.spp}spp_b{args.bounces}"
@@ -152,7 +156,10 @@ def main():
     def step(evs=None):
         if evs is not None:
             evs[0].record(stream)
-        renderer.render(params, out=tile, stream=stream)
+        if args.batch_spp:
+            renderer.render_progressive(params, args.batch_spp, out=tile, stream=stream)
+        else:
+            renderer.render(params, out=tile, stream=stream)
         if evs is not None:
             evs[1].record(stream)
         if world > 1:
@@ -189,6 +196,11 @@ def main():
         total_samples = W * H * spp * args.steps  # all ranks together
         value = total_samples / elapsed / 1e6
         launch_bytes = W * rows * BYTES_PER_PIXEL
+        if args.batch_spp and spp > args.batch_spp:
+            # per step: first batch 20 B/px (seed + sum write), middle batches 36 B/px
+            # (+ sum read), last 52 B/px (+ frame store) — SURVEY §8d
+            nb = -(-spp // args.batch_spp)
+            launch_bytes = W * rows * (20 + 36 * (nb - 2) + 52)
         achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = None
         prof = load_profile_json("pmc_summary.json")

@@ -248,6 +248,33 @@ class Renderer:
                                    ctypes.c_void_p(ptr), ctypes.c_void_p(stream)), self._ctx)
         return out
 
+    def render_progressive(self, params: RenderParams, batch_spp: int, out, stream=None):
+        """Progressive accumulation: ``params.spp`` samples as
+        launches of ``batch_spp`` samples into the context's running fp32 sums
+        (``RT_KEEP_SUM`` / ``accumulate`` with ``sample_base`` advancing), all
+        enqueued on ``stream``; the last launch writes the averaged frame to the
+        device tensor ``out``.  Bit-identical to one launch of ``params.spp``."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream().cuda_stream
+        elif hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        total, done = params.spp, 0
+        ptr = out if isinstance(out, int) else out.data_ptr()
+        while done < total:
+            n = min(batch_spp, total - done)
+            last = done + n == total
+            p = RenderParams(spp=n, bounces=params.bounces, sample_base=params.sample_base + done,
+                             row_start=params.row_start, row_step=params.row_step,
+                             row_count=params.row_count, accumulate=done > 0, keep_sum=True,
+                             fp16=params.fp16)
+            flags = RT_OUT_DEVICE if last else (RT_OUT_DEVICE | RT_OUT_NONE)
+            _check(lib.rt_render_async(self._ctx, ctypes.byref(p.c(flags)),
+                                       ctypes.c_void_p(ptr if last else None),
+                                       ctypes.c_void_p(stream)), self._ctx)
+            done += n
+        return out
+
     def accumulate(self, params: RenderParams):
         """Add samples to the context's running sums only (no image output)."""
         _check(lib.rt_render(self._ctx, ctypes.byref(params.c(RT_OUT_NONE | RT_KEEP_SUM)), None),

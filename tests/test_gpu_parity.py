@@ -209,3 +209,19 @@ def test_random_quads_pair_layout_and_culling_bit_exact(seed):
     with Renderer(s, seeds=sd) as r:
         out = r.render(RenderParams(spp=16, bounces=4))
     assert_parity(out, oracle_lib.render(s, sd, 16, 4), f"quads seed {seed}")
+
+
+def test_render_progressive_async_equals_single_shot():
+    import torch
+    s = Scene.cornell_box(48, 32)
+    with Renderer(s) as r:
+        one = r.render(RenderParams(spp=10, bounces=3))
+        d = torch.empty((32, 48, 4), dtype=torch.float32, device="cuda")
+        r.render_progressive(RenderParams(spp=10, bounces=3), 4, out=d)
+        torch.cuda.synchronize()
+        tiles = torch.empty((11, 48, 4), dtype=torch.float32, device="cuda")
+        r.render_progressive(RenderParams(spp=10, bounces=3, row_start=1, row_step=3), 3,
+                             out=tiles)
+        torch.cuda.synchronize()
+    assert_parity(d.cpu().numpy(), one, "progressive")
+    assert_parity(tiles.cpu().numpy(), one[1::3], "progressive tiles")
