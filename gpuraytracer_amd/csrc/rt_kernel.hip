@@ -114,9 +114,12 @@ struct PathState {
 // One bounce b of raytrace.metal:47-101.  Returns false when the path ends.
 // Shading of a hit (id, t) at bounce b: raytrace.metal:55-101.  Returns false
 // when the path ends (light hit).
-template <int b, int B, int GEO, bool SPH, bool SMALL>
+// FUSE (pair layout, triangles only): the shadow query of bounce b and the
+// closest hit of bounce b+1 run as one pass over the records
+// (fused_shadow_closest); the next hit is returned in *nid / *nt.
+template <int b, int B, int GEO, bool SPH, bool SMALL, bool FUSE = false>
 __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, PathState& s, int id,
-                                      float t) {
+                                      float t, int* nid = nullptr, float* nt = nullptr) {
     f3 N, right, fwd, diffuse;
     if (!SPH || (uint32_t)id < sv.nT) {
         const float4* sh = P.tri_shade + 4 * id;
@@ -162,6 +165,22 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     s.thr = s.thr * diffuse;                               // :76
     const f3 seg_lo{fminf(p.x, q.x), fminf(p.y, q.y), fminf(p.z, q.z)};
     const f3 seg_hi{fmaxf(p.x, q.x), fmaxf(p.y, q.y), fmaxf(p.z, q.z)};
+    if (FUSE && b + 1 < B) {
+        const float cu = halton_dim<4 + 5 * b, SMALL>(s.i);           // :93-94
+        const float cv = halton_dim<5 + 5 * b, SMALL>(s.i);
+        float sp, cp;
+        sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
+        const float ct = sqrtf(cv);
+        const float st = sqrtf(1.0f - ct * ct);
+        const f3 d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
+        const FusedHit h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
+        if (!h.occluded) s.acc = s.acc + lc * s.thr;       // :79-89
+        s.d = d2;
+        s.o = p;                                           // :99-100
+        *nid = h.id;
+        *nt = h.t;
+        return true;
+    }
     if (!any_hit<GEO, SPH, (b == 0 && RT_SPH_PACKET) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + lc * s.thr;                        // :87-89
     if (b + 1 < B) {                                       // last direction never traced
@@ -199,6 +218,37 @@ template <int B, int GEO, bool SPH, bool SMALL>
 struct BounceChain<B, B, GEO, SPH, SMALL> {
     __device__ __forceinline__ static void run(const KParams&, const SceneView&, PathState&) {}
 };
+
+// Fused bounce chain: enters bounce b with the closest hit (id, t) of its ray.
+template <int b, int B, int GEO, bool SMALL>
+struct FusedChain {
+    __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv,
+                                               PathState& s, int id, float t) {
+        int nid = -1;
+        float nt = 0.0f;
+        if (!shade<b, B, GEO, false, SMALL, true>(P, sv, s, id, t, &nid, &nt)) return;
+        if (b + 1 < B && nid >= 0) FusedChain<b + 1, B, GEO, SMALL>::run(P, sv, s, nid, nt);
+    }
+};
+template <int B, int GEO, bool SMALL>
+struct FusedChain<B, B, GEO, SMALL> {
+    __device__ __forceinline__ static void run(const KParams&, const SceneView&, PathState&, int,
+                                               float) {}
+};
+
+#ifndef RT_FUSED
+#define RT_FUSED 1
+#endif
+template <int B, int GEO, bool SPH, bool SMALL>
+__device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv, PathState& s) {
+    if (RT_FUSED && GEO == kGeoPairLds && !SPH && B > 1) {
+        float t = 1000.0f;                                  // sampling.metal:155
+        const int id = closest_hit<GEO, false, true, 0>(sv, s.o, s.d, 0.001f, &t);
+        if (id >= 0) FusedChain<0, B, GEO, SMALL>::run(P, sv, s, id, t);
+    } else {
+        BounceChain<0, B, GEO, SPH, SMALL>::run(P, sv, s);
+    }
+}
 
 // ---- sorted-path variant ----------------------------------------------------
 // Between bounces the 256 paths of a workgroup are counting-sorted through LDS
@@ -381,7 +431,7 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
         s.o = ld_f3(P.cam_pos);
         s.acc = f3{0.0f, 0.0f, 0.0f};
         s.thr = f3{1.0f, 1.0f, 1.0f};
-        BounceChain<0, B, GEO, SPH, SMALL>::run(P, sv, s);                  // :47-102
+        trace_path<B, GEO, SPH, SMALL>(P, sv, s);                           // :47-102
         lum = lum + s.acc;                                       // :103
     }
     if (P.sum) P.sum[o] = make_float4(lum.x, lum.y, lum.z, (float)P.samples_total);

@@ -399,5 +399,67 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
     return false;
 }
 
+// Fused queries of one bounce (pair layout, triangles only): the shadow any-hit
+// of bounce b from p toward the light sample, and the closest hit of bounce
+// b+1 from the same p along the new direction d2.  Both are evaluated pair by
+// pair over ONE load of each record; every lane's two results are exactly
+// those of any_hit and closest_hit (same tests, same order, same culling rule
+// for the shadow segment), so the path's arithmetic is unchanged.
+struct FusedHit {
+    bool occluded;
+    int id;     // closest hit of (p, d2), -1 if none
+    float t;
+};
+
+__device__ __forceinline__ FusedHit fused_shadow_closest(const SceneView& sv, f3 p, f3 L,
+                                                         float smax, f3 seg_lo, f3 seg_hi,
+                                                         f3 d2) {
+    FusedHit h{false, -1, 1000.0f};  // max_distance (sampling.metal:155)
+    for (uint32_t k = 0; k < sv.nP; ++k) {
+        const float4* r = sv.pair + kPairF4 * k;
+        const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+        // shadow ray: segment-box cull, then the any-hit test for lanes still open
+        const float4 b0 = r[5], b1 = r[6];
+        const bool overlap = !h.occluded && seg_lo.x <= b0.w && seg_hi.x >= b0.x &&
+                             seg_lo.y <= b1.x && seg_hi.y >= b0.y && seg_lo.z <= b1.y &&
+                             seg_hi.z >= b0.z;
+        if (__any(overlap)) {
+            const PairDots q = pair_dots(r0, r1, r2, r3, r4, p, L);
+            const bool pa = overlap && bary_ok(q.denA, q.a1, q.a2);
+            const bool pb = overlap && bary_ok(q.denB, q.b1, q.b2);
+            if (pa || pb) {
+                const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+                const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
+                bool hit = t > 0.0f && t < smax;
+                if (pa && pb && !hit) {
+                    const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
+                    hit = t2 > 0.0f && t2 < smax;
+                }
+                h.occluded = h.occluded || hit;
+            }
+        }
+        // next-bounce closest hit (no culling: bounce rays are incoherent)
+        const PairDots q = pair_dots(r0, r1, r2, r3, r4, p, d2);
+        const bool pa = bary_ok(q.denA, q.a1, q.a2);
+        const bool pb = bary_ok(q.denB, q.b1, q.b2);
+        if (pa || pb) {
+            const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+            const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
+            if (t > 0.001f && t < h.t) {
+                h.t = t;
+                h.id = (int)(pa ? 2 * k : 2 * k + 1);
+            }
+            if (pa && pb) {
+                const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
+                if (t2 > 0.001f && t2 < h.t) {
+                    h.t = t2;
+                    h.id = (int)(2 * k + 1);
+                }
+            }
+        }
+    }
+    return h;
+}
+
 }  // namespace
 }  // namespace rt
