@@ -80,6 +80,32 @@ def test_spheres_1000_vs_oracle():
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), "spheres1000")
 
 
+@pytest.mark.parametrize("leaf", ["2", "3", "8"])
+def test_sphere_bvh_multi_sphere_leaves(leaf, monkeypatch):
+    # RTPT_BVH_LEAF > 1: leaves hold several spheres (the default is one per leaf)
+    monkeypatch.setenv("RTPT_BVH_LEAF", leaf)
+    s = Scene.random_spheres(40, 24, 700, seed=5)
+    sd = seed_splitmix(40, 24)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=2, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, 2, 3), "leaf" + leaf)
+
+
+def test_duplicate_spheres_tie_to_lower_id():
+    # exact duplicates (same centre and radius, different albedo) hit at the same t:
+    # the BVH walks must return the lower sphere id, as the id-ordered scan does
+    s = Scene.random_spheres(40, 24, 300, seed=11)
+    n = s.n_spheres
+    for k in range(0, n - 1, 2):
+        s.spheres[k + 1].center = s.spheres[k].center
+        s.spheres[k + 1].radius = s.spheres[k].radius
+        s.spheres[k + 1].material.diffuse.x = 0.05 + 0.9 * ((k * 37) % 17) / 17.0
+    sd = seed_splitmix(40, 24)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=2, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, 2, 3), "duplicates")
+
+
 def test_large_sphere_scene_bvh():
     # 5000 spheres: deep BVH (2047 nodes), ties and leaves far beyond the 1000-sphere case
     s = Scene.random_spheres(24, 16, 5000, seed=9)
