@@ -8,6 +8,10 @@
 // hard-coded constants (raytrace.metal:24-25, scene.swift:18, renderer.swift:100):
 //   rtrace [out.png] [--res WxH] [--spp N] [--batch N] [--bounces B]
 //          [--scene cornell|spheres:N] [--seed KEY] [--device D] [--pfm out.pfm]
+//   rtrace --mis [out.png] [--res WxH] [--camera-rays N] [--mis-samples N]
+//          the SwiftPM build (Sources/gpuRaytracer/main.swift:96-108): scene with the
+//          1.5 x 1.5 light, kernel drawTriangle (6 camera rays x 300 MIS samples),
+//          its own tonemapped RGBA8 written as the PNG
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -108,6 +112,8 @@ class Renderer {
         uint32_t spheres = 0;             // 0 = Cornell box
         uint64_t seed_key = 0x5EED00000000ull;
         int device = 0;
+        bool mis = false;                 // SwiftPM drawTriangle instead of pathTrace
+        uint32_t camera_rays = 6, mis_samples = 300;  // shaders.metal:644-649
     };
 
     explicit Renderer(const Options& o) : opt_(o) {  // Renderer.init() :29-115
@@ -120,6 +126,11 @@ class Renderer {
             spheres_.resize(o.spheres);
             rt_scene_random_spheres(o.width, o.height, o.spheres, 42, &camera_, mats.data(),
                                     verts.data(), &light_, &n_tri, spheres_.data());
+        } else if (o.mis) {
+            mats.resize(RT_CORNELL_TRIANGLES);
+            verts.resize(3 * RT_CORNELL_TRIANGLES);
+            rt_scene_cornell_box_mis(o.width, o.height, &camera_, mats.data(), verts.data(),
+                                     &light_, &n_tri);
         } else {
             mats.resize(RT_CORNELL_TRIANGLES);
             verts.resize(3 * RT_CORNELL_TRIANGLES);
@@ -164,6 +175,21 @@ class Renderer {
         return kernel_s;
     }
 
+    // drawTriangle(device:...) (Sources/gpuRaytracer/computeShader.swift:99-189):
+    // radiance sums and the kernel's own RGBA8; returns kernel seconds
+    double draw_mis(std::vector<float>* sums, std::vector<uint8_t>* rgba8) {
+        sums->assign((size_t)opt_.width * opt_.height * 4, 0.0f);
+        rgba8->assign((size_t)opt_.width * opt_.height * 4, 0);
+        rt_mis_params p;
+        memset(&p, 0, sizeof(p));
+        p.camera_rays = opt_.camera_rays;
+        p.mis_samples = opt_.mis_samples;
+        check(rt_render_mis(ctx_, &p, sums->data(), rgba8->data()), ctx_);
+        float ms = 0;
+        check(rt_last_kernel_ms(ctx_, &ms), ctx_);
+        return ms * 1e-3;
+    }
+
    private:
     static void check(int s, rt_ctx* c) {
         if (s != RT_OK) {
@@ -197,6 +223,9 @@ int main(int argc, char** argv) {
         else if (a == "--seed") o.seed_key = strtoull(next(), nullptr, 0);
         else if (a == "--device") o.device = atoi(next());
         else if (a == "--pfm") pfm = next();
+        else if (a == "--mis") o.mis = true;
+        else if (a == "--camera-rays") o.camera_rays = (uint32_t)strtoul(next(), nullptr, 10);
+        else if (a == "--mis-samples") o.mis_samples = (uint32_t)strtoul(next(), nullptr, 10);
         else if (a == "--scene") {
             const std::string s = next();
             if (s.rfind("spheres:", 0) == 0) o.spheres = (uint32_t)strtoul(s.c_str() + 8, nullptr, 10);
@@ -204,7 +233,25 @@ int main(int argc, char** argv) {
         } else if (a.size() && a[0] != '-') out = a;
         else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
+    if (o.mis && o.spheres) { fprintf(stderr, "--mis renders the SwiftPM Cornell scene only\n"); return 2; }
     Renderer r(o);
+    if (o.mis) {  // Sources/gpuRaytracer/main.swift:96-108
+        std::vector<float> sums;
+        std::vector<uint8_t> rgba8;
+        const auto t0 = std::chrono::steady_clock::now();
+        const double ks = r.draw_mis(&sums, &rgba8);
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (!write_png(out.c_str(), rgba8.data(), o.width, o.height)) {
+            fprintf(stderr, "failed to write %s\n", out.c_str());
+            return 1;
+        }
+        if (!pfm.empty() && !write_pfm(pfm.c_str(), sums.data(), o.width, o.height)) return 1;
+        printf("Image saved to: %s\n", out.c_str());  // image.swift:89
+        printf("Render completed in %.2f seconds\n", wall);  // main.swift:106
+        printf("{\"res\": \"%dx%d\", \"camera_rays\": %u, \"mis_samples\": %u, \"kernel_s\": %.6f}\n",
+               o.width, o.height, o.camera_rays, o.mis_samples, ks);
+        return 0;
+    }
     std::vector<float> img;
     const auto t0 = std::chrono::steady_clock::now();
     const double ks = r.draw(&img);
