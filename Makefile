@@ -14,7 +14,7 @@ HOSTCXX ?= /opt/rocm/llvm/bin/clang++
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-slp-vectorize
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include
 
-OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
+OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
 HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp
 
 all: $(PKG)/librtpt.so $(PKG)/rtrace oracle

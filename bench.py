@@ -42,12 +42,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres", "triangles"])
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=256, help="samples per pixel per GPU")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--spheres", type=int, default=1000)
+    ap.add_argument("--triangles", type=int, default=100000,
+                    help="random triangles added to the room for --scene triangles")
     ap.add_argument("--batch-spp", type=int, default=0,
                     help="progressive mode: launches of this many spp into a running sum")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
@@ -140,9 +142,12 @@ def main():
         workload = f"cornell_{W}x{H}_{args.spp}spp_b{args.bounces}"
         if args.batch_spp:
             workload += f"_progressive{args.batch_spp}"
-    else:
+    elif args.scene == "spheres":
         scene = Scene.random_spheres(W, H, args.spheres, seed=42)
         workload = f"spheres{args.spheres}_{W}x{H}_{args.spp}spp_b{args.bounces}"
+    else:
+        scene = Scene.random_triangles(W, H, args.triangles, seed=7)
+        workload = f"triangles{args.triangles}_{W}x{H}_{args.spp}spp_b{args.bounces}"
     renderer = Renderer(scene, device=local)
     row_start, row_step, rows = rank_rows(H, world, rank)
     spp = args.spp * world  # weak scaling: W*H*spp samples per GPU whatever N
@@ -228,7 +233,9 @@ def main():
             "data": ("synthetic: reference Cornell scene (scene.swift), splitmix64 seeds"
                      if args.scene == "cornell" else
                      f"synthetic: {args.spheres} PCG32 spheres (seed 42) in the Cornell room, "
-                     "splitmix64 seeds"),
+                     "splitmix64 seeds" if args.scene == "spheres" else
+                     f"synthetic: {args.triangles} random triangles (PCG64 seed 7) in the "
+                     "Cornell room, splitmix64 seeds"),
             "config": {"workload": workload, "width": W, "height": H, "spp_per_gpu": args.spp,
                        "spp_frame": spp, "bounces": args.bounces,
                        "parallelism": (f"{world} row-interleaved tiles + 1 RCCL gather" if world > 1

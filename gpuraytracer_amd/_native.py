@@ -87,7 +87,7 @@ class RenderParamsC(ctypes.Structure):  # rt_render_params
 class SceneInfo(ctypes.Structure):  # rt_scene_info
     _fields_ = [(n, ctypes.c_uint32) for n in
                 ("n_triangles", "n_triangle_pairs", "n_spheres", "lds_bytes",
-                 "n_sphere_nodes")]
+                 "n_sphere_nodes", "n_triangle_bvh_nodes")]
 
 
 RT_OK = 0

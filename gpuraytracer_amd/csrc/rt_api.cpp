@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <string>
 #include <vector>
@@ -31,6 +32,10 @@ struct rt_ctx {
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
     uint32_t* d_sph_perm = nullptr;
+    float4* d_tri_nodes = nullptr;   // GPU-built triangle BVH (rt_lbvh.hip)
+    float4* d_tri_sorted = nullptr;
+    uint32_t* d_tri_perm = nullptr;
+    uint32_t tri_bvh_nodes = 0;      // per layout
     float4* d_mis_shade = nullptr;
     float4* d_mis_tab = nullptr;   // Halton table of the MIS integrator
     uint32_t mis_tab_S = 0;        // samples per strategy it was built for
@@ -47,7 +52,7 @@ struct rt_ctx {
     size_t out_cap = 0;     // bytes
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
-    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|sorted (tuning knob)
+    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|pairsmem|sorted|bvh (tuning knob)
     std::string err;
 };
 
@@ -101,6 +106,9 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_sph_nodes);
     (void)hipFree(c->d_sph_perm);
+    (void)hipFree(c->d_tri_nodes);
+    (void)hipFree(c->d_tri_sorted);
+    (void)hipFree(c->d_tri_perm);
     (void)hipFree(c->d_mis_shade);
     (void)hipFree(c->d_mis_tab);
     (void)hipFree(c->d_out8);
@@ -189,6 +197,10 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.sph_shade = c->d_sph_shade;
     K.sph_nodes = c->d_sph_nodes;
     K.sph_perm = c->d_sph_perm;
+    K.tri_nodes = c->d_tri_nodes;
+    K.tri_sorted = c->d_tri_sorted;
+    K.tri_perm = c->d_tri_perm;
+    K.nTN = c->tri_bvh_nodes;
     K.seeds = c->d_seeds;
     K.sum = (keep_sum || p->accumulate) ? c->d_sum : nullptr;
     K.out = kout;
@@ -343,6 +355,10 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
     K.pair_isect = c->d_pair_isect;
     K.mis_shade = c->d_mis_shade;
     K.u_tab = c->d_mis_tab;
+    K.tri_nodes = c->d_tri_nodes;
+    K.tri_sorted = c->d_tri_sorted;
+    K.tri_perm = c->d_tri_perm;
+    K.nTN = c->tri_bvh_nodes;
     K.out = kout;
     K.out8 = kout8;
     K.nT = (uint32_t)c->scene.tri_isect.size();
@@ -434,6 +450,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
         if (!strcmp(m, "sorted")) c->scene_mem = rt::SceneMem::kPairSorted;
         if (!strcmp(m, "pairsmem")) c->scene_mem = rt::SceneMem::kPairSmem;
+        if (!strcmp(m, "bvh")) c->scene_mem = rt::SceneMem::kTriBvh;
     }
     DeviceGuard g(c->device);
     const char* err = nullptr;
@@ -461,6 +478,30 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
             (e = upload(&c->d_sph_perm, s.sph_perm.data(), s.sph_perm.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_mis_shade, s.mis_shade.data(), s.mis_shade.size() * sizeof(rt::MisShade), c->stream)) != hipSuccess) {
             status = RT_ERR_OUT_OF_MEMORY; msg = std::string("scene upload: ") + hipGetErrorString(e); break;
+        }
+        // Triangle BVH, built on the device (replaces setupAccelerationStructures,
+        // computeShader.swift:45-97): above kTriBvhMinTriangles or when the records
+        // do not fit the LDS layouts, or when forced (RTPT_SCENE_MEM=bvh).
+        const uint32_t nT = (uint32_t)s.tri_isect.size();
+        const size_t lds_pairs = rt::kernel_lds_bytes(nT, (uint32_t)s.pair_isect.size(), 0, 0);
+        const size_t lds_single = rt::kernel_lds_bytes(nT, 0, 0, 0);
+        const bool need_bvh = nT > 0 && (c->scene_mem == rt::SceneMem::kTriBvh ||
+                                         (c->scene_mem == rt::SceneMem::kAuto &&
+                                          (nT > rt::kTriBvhMinTriangles ||
+                                           std::min(lds_pairs, lds_single) > rt::kMaxLdsBytes)));
+        if (need_bvh) {
+            const size_t nn = 2 * (size_t)nT - 1;
+            if ((e = hipMalloc((void**)&c->d_tri_nodes, 8 * nn * 2 * sizeof(float4))) != hipSuccess ||
+                (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
+                (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
+                status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;
+            }
+            if ((e = rt::build_tri_lbvh(c->d_tri_isect, nT, s.tri_lo, s.tri_hi, s.margin, c->d_tri_nodes,
+                                        c->d_tri_sorted, c->d_tri_perm, c->stream)) != hipSuccess) {
+                status = (e == hipErrorInvalidValue) ? RT_ERR_INVALID_ARG : RT_ERR_LAUNCH;
+                msg = std::string("triangle BVH build: ") + hipGetErrorString(e); break;
+            }
+            c->tri_bvh_nodes = (uint32_t)nn;
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
         if ((e = hipMalloc((void**)&c->d_seeds, npx * sizeof(uint32_t))) != hipSuccess) {
@@ -549,7 +590,11 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     info->n_sphere_nodes = s.sph_layout_nodes;
     const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres,
                                             s.sph_layout_nodes);
-    info->lds_bytes = lds <= rt::kMaxLdsBytes ? (uint32_t)lds : 0u;
+    const size_t lds_single = rt::kernel_lds_bytes(info->n_triangles, 0, 0, 0);
+    const bool bvh = info->n_triangles > rt::kTriBvhMinTriangles ||
+                     std::min(lds, lds_single) > rt::kMaxLdsBytes;
+    info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
+    info->lds_bytes = (!bvh && lds <= rt::kMaxLdsBytes) ? (uint32_t)lds : 0u;
     return RT_OK;
 }
 

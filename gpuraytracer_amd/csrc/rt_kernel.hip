@@ -399,6 +399,10 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
     }
+    sv.tnode = P.tri_nodes;
+    sv.tsorted = P.tri_sorted;
+    sv.tperm = P.tri_perm;
+    sv.nTN = P.nTN;
     sv.node = P.sph_nodes;  // sphere BVH: scalar loads from global memory
     sv.sph = P.sph_isect;
     sv.nN = SPH ? P.nN : 0u;
@@ -463,6 +467,10 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
     float4* scene = lds + kSortF4;  // sort buffers first: compile-time offsets
     for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) scene[k] = P.pair_isect[k];
     sv.nN = SPH ? P.nN : 0u;
+    sv.tnode = P.tri_nodes;
+    sv.tsorted = P.tri_sorted;
+    sv.tperm = P.tri_perm;
+    sv.nTN = P.nTN;
     sv.tri = scene;
     sv.pair = scene;
     sv.node = P.sph_nodes;
@@ -541,7 +549,8 @@ template <int B, int GEO, bool SPH, bool SMALL>
 hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(kBlockThreads),
-                       (GEO == kGeoTriGlobal || GEO == kGeoPairSmem) ? 0 : lds_bytes, stream, P);
+                       (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,
+                       stream, P);
     return hipGetLastError();
 }
 
@@ -579,6 +588,7 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
     switch (geo) {
         case kGeoPairLds: return launch_g<B, kGeoPairLds>(P, lds_bytes, stream);
         case kGeoPairSmem: return launch_g<B, kGeoPairSmem>(P, lds_bytes, stream);
+        case kGeoTriBvh: return launch_g<B, kGeoTriBvh>(P, lds_bytes, stream);
         case kGeoTriLds: return launch_g<B, kGeoTriLds>(P, lds_bytes, stream);
         default: return launch_g<B, kGeoTriGlobal>(P, lds_bytes, stream);
     }
@@ -600,6 +610,9 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
     int geo = kGeoTriGlobal;
     if (mem != SceneMem::kSmem && lds_bytes <= kMaxLdsBytes) geo = pairs ? kGeoPairLds : kGeoTriLds;
     if (mem == SceneMem::kPairSmem && P.nP > 0) geo = kGeoPairSmem;
+    // triangle BVH whenever rt_create built one (kTriBvhMinTriangles or no LDS fit),
+    // unless another layout is forced
+    if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) geo = kGeoTriBvh;
     // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the
     // Cornell 1080p workload (barrier + occupancy cost).
     if (geo == kGeoPairLds && mem == SceneMem::kPairSorted &&

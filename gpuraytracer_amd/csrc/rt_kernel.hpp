@@ -14,6 +14,9 @@ constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
 constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
+// Above this many triangles rt_create builds the triangle BVH (measured crossover
+// of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
+constexpr uint32_t kTriBvhMinTriangles = 384;
 
 // Kernel arguments (passed by value -> kernarg segment / SGPRs).
 struct KParams {
@@ -24,10 +27,14 @@ struct KParams {
     const float4* sph_nodes;  // 2 float4 per sphere-BVH node (BvhNode)
     const uint32_t* sph_perm; // BVH leaf order -> sphere id
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
+    const float4* tri_nodes;  // triangle BVH (rt_lbvh.hip): 8 layouts x nTN nodes, or null
+    const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
+    const uint32_t* tri_perm; // BVH leaf order -> triangle id
     const uint32_t* seeds;    // W*H, full frame
     float4* sum;              // running sums (tile layout) or null
     void* out;                // rgba32F / rgba16F tile or null
     uint32_t nT, nP, nS, nN;  // triangles, triangle pairs (0: no pair layout), spheres, BVH nodes
+    uint32_t nTN;             // triangle-BVH nodes per layout (0: no triangle BVH)
     float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
     float halfW, halfH;
     int32_t W, H;
@@ -42,13 +49,17 @@ struct KParams {
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);
 // Where the workgroup reads the intersection records from.
-enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4 };
+enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
 hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
 // Arguments of the MIS integrator kernel (rt_mis.hip; Sources/gpuRaytracer/
 // shaders.metal:635-707).
 struct MisParams {
     const float4* tri_isect;   // 3 float4 per triangle
+    const float4* tri_nodes;   // triangle BVH or null (as KParams)
+    const float4* tri_sorted;
+    const uint32_t* tri_perm;
+    uint32_t nTN;
     const float4* pair_isect;  // kPairF4 float4 per pair, or null
     const float4* mis_shade;   // 3 float4 per triangle (MisShade)
     const float4* u_tab;       // 3 float4 per MIS sample index i < S (Halton table)
@@ -65,6 +76,12 @@ struct MisParams {
 };
 hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream);
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs);
+
+// GPU build of the triangle BVH (rt_lbvh.hip).  d_nodes: 8 * (2n-1) * 2 float4,
+// d_sorted: 3n float4, d_perm: n.  Synchronises the stream.
+hipError_t build_tri_lbvh(const float4* d_tri, uint32_t n, const float lo[3], const float hi[3],
+                          float margin, float4* d_nodes, float4* d_sorted, uint32_t* d_perm,
+                          hipStream_t s);
 
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 

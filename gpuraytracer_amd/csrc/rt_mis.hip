@@ -274,7 +274,14 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     sv.node = nullptr;
     sv.sph = nullptr;
     sv.sph_perm = nullptr;
-    if (GEO != kGeoTriGlobal) {
+    sv.tnode = P.tri_nodes;
+    sv.tsorted = P.tri_sorted;
+    sv.tperm = P.tri_perm;
+    sv.nTN = P.nTN;
+    if (GEO == kGeoTriBvh) {
+        sv.tri = nullptr;
+        sv.pair = nullptr;
+    } else if (GEO != kGeoTriGlobal) {
         const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
@@ -349,7 +356,10 @@ hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
     const bool pairs = mem != SceneMem::kLdsSingle && P.nP > 0;
     const size_t lds = mis_lds_bytes(P.nT, pairs ? P.nP : 0u);
-    if (mem != SceneMem::kSmem && lds <= kMaxLdsBytes) {
+    const bool lds_ok = mem != SceneMem::kSmem && lds <= kMaxLdsBytes;
+    if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) {
+        hipLaunchKernelGGL(mis_kernel<kGeoTriBvh>, grid, dim3(kBlockThreads), 0, stream, P);
+    } else if (lds_ok) {
         if (pairs)
             hipLaunchKernelGGL(mis_kernel<kGeoPairLds>, grid, dim3(kBlockThreads), lds, stream, P);
         else

@@ -504,6 +504,18 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                                4e-5f * fmaxf(fabsf(cam.position.x),
                                              fmaxf(fabsf(cam.position.y), fabsf(cam.position.z))));
     build_pairs(out, verts, margin);
+    out->margin = margin;
+    for (int a = 0; a < 3; ++a) {
+        out->tri_lo[a] = INFINITY;
+        out->tri_hi[a] = -INFINITY;
+    }
+    for (uint32_t k = 0; k < 3 * n_tri; ++k) {
+        const float c[3] = {verts[k].x, verts[k].y, verts[k].z};
+        for (int a = 0; a < 3; ++a) {
+            out->tri_lo[a] = fminf(out->tri_lo[a], c[a]);
+            out->tri_hi[a] = fmaxf(out->tri_hi[a], c[a]);
+        }
+    }
     out->sph_shade.resize(n_sph);
     build_sphere_bvh(out, spheres, n_sph, margin);
     for (uint32_t k = 0; k < n_sph; ++k) {

@@ -97,6 +97,8 @@ struct CompiledScene {
     std::vector<BvhNode> sph_nodes;     // 8 octant layouts of sph_layout_nodes nodes each
     uint32_t sph_layout_nodes = 0;
     std::vector<SphShade> sph_shade;    // by sphere id
+    float tri_lo[3], tri_hi[3];         // bounds of the triangle vertices (BVH build)
+    float margin = 0.0f;                // culling margin
     MisLightConst mis_light;
     std::vector<MisShade> mis_shade;    // by triangle id
 };

@@ -133,6 +133,7 @@ enum Geo : int {
     kGeoTriLds = 0,     // single-triangle records staged in LDS
     kGeoPairLds = 1,    // shared-edge pair records staged in LDS
     kGeoPairSmem = 4,   // shared-edge pair records read with scalar loads (no LDS)
+    kGeoTriBvh = 5,     // GPU-built triangle BVH (rt_lbvh.hip), records from global
     kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
 };
 
@@ -144,6 +145,10 @@ struct SceneView {
     const float4* sph;        // 1 float4 per sphere, BVH leaf order
     const float4* node;       // 2 float4 per sphere-BVH node
     const uint32_t* sph_perm; // leaf order -> sphere id (global memory)
+    const float4* tnode;      // triangle BVH: 8 octant layouts of nTN nodes
+    const float4* tsorted;    // 3 float4 per triangle, BVH leaf order
+    const uint32_t* tperm;    // leaf order -> triangle id
+    uint32_t nTN;
     uint32_t nT, nP, nS, nN;
 };
 
@@ -282,6 +287,93 @@ __device__ __forceinline__ bool sphere_any(const float4* __restrict__ node,
     return found;
 }
 
+// Triangle-BVH walks: the sphere walks above with the triangle test in the
+// leaves (one triangle per leaf) — same conservative boxes, same (t, id)
+// ranking, so the result is the id-ordered brute-force scan's.
+template <bool PACKET>
+__device__ __forceinline__ void tri_bvh_closest(const float4* __restrict__ node,
+                                                const float4* __restrict__ tri,
+                                                const uint32_t* __restrict__ perm, uint32_t nN,
+                                                f3 o, f3 d, float tmin, float& best, int& id) {
+    const RayBox rb = ray_box(o, d);
+    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
+    uint32_t idx = 0;
+    while (idx < nN) {
+        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
+        uint32_t next = PACKET ? wave_uniform(__float_as_uint(n0.w)) : __float_as_uint(n0.w);
+        const bool h = node_hit(n0, n1, rb, tmin, best);
+        if (PACKET ? __builtin_amdgcn_ballot_w64(h) != 0 : h) {
+            const uint32_t leaf = PACKET ? wave_uniform(__float_as_uint(n1.w)) : __float_as_uint(n1.w);
+            if (leaf == 0u) {
+                next = idx + 1;
+            } else {
+                const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                for (uint32_t k = first; k < end; ++k) {
+                    float t;
+                    if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f,
+                                 &t) && t <= best) {
+                        const int tid = (int)perm[k];
+                        if (t < best || tid < id) {
+                            best = t;
+                            id = tid;
+                        }
+                    }
+                }
+            }
+        }
+        idx = next;
+    }
+}
+
+template <bool PACKET>
+__device__ __forceinline__ bool tri_bvh_any(const float4* __restrict__ node,
+                                            const float4* __restrict__ tri, uint32_t nN, f3 o,
+                                            f3 d, float tmin, float tmax) {
+    const RayBox rb = ray_box(o, d);
+    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
+    bool found = false;
+    uint32_t idx = 0;
+    while (idx < nN) {
+        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
+        if (PACKET) {
+            uint32_t next = wave_uniform(__float_as_uint(n0.w));
+            if (__builtin_amdgcn_ballot_w64(!found && node_hit(n0, n1, rb, tmin, tmax)) != 0) {
+                const uint32_t leaf = wave_uniform(__float_as_uint(n1.w));
+                if (leaf == 0u) {
+                    next = idx + 1;
+                } else {
+                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                    for (uint32_t k = first; k < end; ++k) {
+                        float t;
+                        found = found || tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d,
+                                                  tmin, tmax, &t);
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
+                }
+            }
+            idx = next;
+        } else {
+            uint32_t next = __float_as_uint(n0.w);
+            if (node_hit(n0, n1, rb, tmin, tmax)) {
+                const uint32_t leaf = __float_as_uint(n1.w);
+                if (leaf == 0u) {
+                    next = idx + 1;
+                } else {
+                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                    for (uint32_t k = first; k < end; ++k) {
+                        float t;
+                        if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax,
+                                     &t))
+                            return true;
+                    }
+                }
+            }
+            idx = next;
+        }
+    }
+    return found;
+}
+
 // closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
 // Primitives are tested in id order; a strictly smaller t wins (ties keep the
 // lower id), exactly as the oracle.
@@ -339,6 +431,8 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
                 }
             }
         }
+    } else if (GEO == kGeoTriBvh) {
+        tri_bvh_closest<CULL>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin, best, id);
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
             float t;
@@ -387,6 +481,8 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
                 }
             }
         }
+    } else if (GEO == kGeoTriBvh) {
+        if (tri_bvh_any<PACKET>(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax)) return true;
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
             float t;

@@ -115,6 +115,29 @@ class Scene:
                                            ctypes.byref(n), sph))
         return cls(cam, mats, verts, light, sph if n_spheres else None)
 
+    @classmethod
+    def random_triangles(cls, width: int = 1920, height: int = 1080, n: int = 100_000,
+                         seed: int = 7, size: float = 0.25) -> "Scene":
+        """Stress scene for the triangle BVH: the Cornell room (ids 0-35, light
+        34-35) plus ``n`` random small triangles (ids 36..) inside it, diffuse
+        albedo in [0.1, 0.9] (numpy PCG64 ``seed``)."""
+        base = cls.cornell_box(width, height)
+        rng = np.random.default_rng(seed)
+        mats = (MaterialGPU * (36 + n))()
+        verts = (float3 * (3 * (36 + n)))()
+        ctypes.memmove(ctypes.addressof(mats), ctypes.addressof(base.materials), 36 * 48)
+        ctypes.memmove(ctypes.addressof(verts), ctypes.addressof(base.vertices), 108 * 16)
+        c = rng.uniform(-2.3, 2.3, size=(n, 1, 3)).astype(np.float32)
+        e = rng.uniform(-size, size, size=(n, 2, 3)).astype(np.float32)
+        tri = np.concatenate([c, c + e], axis=1).reshape(-1, 3)          # v0, v0+a, v0+b
+        vv = np.frombuffer(verts, np.float32).reshape(-1, 4)
+        vv[108:, :3] = tri
+        mm = np.frombuffer(mats, np.float32).reshape(-1, 12)
+        mm[36:, 0:3] = rng.uniform(0.1, 0.9, size=(n, 3)).astype(np.float32)
+        mm[36:, 3] = 1.0
+        mm[36:, 5] = 0.5
+        return cls(base.camera, mats, verts, base.light)
+
     def describe(self) -> dict:
         """Device layout rt_create would choose (rt_scene_describe)."""
         info = SceneInfo()

@@ -183,7 +183,8 @@ typedef struct rt_scene_info {
     uint32_t n_triangle_pairs;   /* >0: every (2k,2k+1) shares v0 and an edge -> pair records */
     uint32_t n_spheres;
     uint32_t lds_bytes;          /* intersection records staged per workgroup (0: read from global) */
-    uint32_t n_sphere_nodes;     /* sphere BVH nodes (32 B each, staged with the records) */
+    uint32_t n_sphere_nodes;     /* sphere BVH nodes per layout (32 B each, 8 layouts, global) */
+    uint32_t n_triangle_bvh_nodes; /* GPU-built triangle BVH nodes per layout (0: LDS layouts) */
 } rt_scene_info;
 int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
 

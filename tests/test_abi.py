@@ -77,7 +77,9 @@ def test_seed_helper_range():
 def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.cornell_box(64, 48).describe()
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
-                    "lds_bytes": 18 * 112, "n_sphere_nodes": 0}
+                    "lds_bytes": 18 * 112, "n_sphere_nodes": 0, "n_triangle_bvh_nodes": 0}
+    soup = g.Scene.random_triangles(16, 8, 1000).describe()
+    assert soup["n_triangle_bvh_nodes"] == 2 * 1036 - 1 and soup["lds_bytes"] == 0
 
     def bvh_nodes(n):  # median split, one sphere per leaf (rt_scene.cpp BvhBuild)
         return 1 if n <= 1 else 1 + bvh_nodes(n // 2) + bvh_nodes(n - n // 2)

@@ -186,7 +186,7 @@ def test_errors_are_status_codes():
         assert out.shape == (8, 16, 4)
 
 
-@pytest.mark.parametrize("layout", ["single", "smem", "sorted", "pairsmem"])
+@pytest.mark.parametrize("layout", ["single", "smem", "sorted", "pairsmem", "bvh"])
 def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
     """The single-triangle LDS layout, the global (scalar-load) layout and the
     octant-sorted path kernel give the same bits as the default pair kernel
@@ -251,3 +251,62 @@ def test_render_progressive_async_equals_single_shot():
         torch.cuda.synchronize()
     assert_parity(d.cpu().numpy(), one, "progressive")
     assert_parity(tiles.cpu().numpy(), one[1::3], "progressive tiles")
+
+
+def triangle_soup(w, h, n, seed, dup=False):
+    """Cornell room + n random small triangles (ids 36..): beyond the LDS layouts,
+    so rt_create builds the triangle BVH on the GPU (rt_lbvh.hip)."""
+    base = Scene.cornell_box(w, h)
+    rng = np.random.default_rng(seed)
+    mats = (MaterialGPU * (36 + n))()
+    verts = (float3 * (3 * (36 + n)))()
+    ctypes_memmove(mats, base.materials, 36 * 48)
+    ctypes_memmove(verts, base.vertices, 108 * 16)
+    c = rng.uniform(-2.3, 2.3, size=(n, 3)).astype(np.float32)
+    if dup:  # every odd triangle repeats the previous one (ties at equal t)
+        c[1::2] = c[0::2][: len(c[1::2])]
+    for k in range(n):
+        e = rng.uniform(-0.25, 0.25, size=(2, 3)).astype(np.float32)
+        if dup and k % 2 == 1:
+            pv = [verts[3 * (36 + k - 1) + j] for j in range(3)]
+            for j in range(3):
+                verts[3 * (36 + k) + j].x, verts[3 * (36 + k) + j].y, verts[3 * (36 + k) + j].z = pv[j].x, pv[j].y, pv[j].z
+        else:
+            for j, p in enumerate((c[k], c[k] + e[0], c[k] + e[1])):
+                verts[3 * (36 + k) + j].x, verts[3 * (36 + k) + j].y, verts[3 * (36 + k) + j].z = (float(v) for v in p)
+        m = mats[36 + k]
+        m.diffuse.x, m.diffuse.y, m.diffuse.z = (float(v) for v in rng.uniform(0.1, 0.9, 3))
+        m.diffuse.w = 1.0
+        m.roughness = 0.5
+    return Scene(base.camera, mats, verts, base.light)
+
+
+def ctypes_memmove(dst, src, n):
+    import ctypes
+    ctypes.memmove(ctypes.addressof(dst), ctypes.addressof(src), n)
+
+
+@pytest.mark.parametrize("n,dup", [(3000, False), (2500, True)])
+def test_triangle_bvh_gpu_build_bit_exact(n, dup):
+    s = triangle_soup(40, 24, n, seed=n, dup=dup)
+    assert s.describe()["lds_bytes"] == 0  # does not fit LDS: the BVH path
+    sd = seed_splitmix(40, 24)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=2, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"soup{n}")
+
+
+def test_triangle_bvh_forced_on_cornell_and_mis(monkeypatch):
+    monkeypatch.setenv("RTPT_SCENE_MEM", "bvh")
+    s = Scene.cornell_box(64, 48)
+    sd = seed_splitmix(64, 48)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=3, bounces=4))
+    assert_parity(out, oracle_lib.render(s, sd, 3, 4), "bvh cornell")
+    from gpuraytracer_amd import MisParams
+    m = Scene.cornell_box_mis(40, 24)
+    with Renderer(m) as r:
+        got, got8 = r.render_mis(MisParams(camera_rays=2, mis_samples=12))
+    ref, ref8 = oracle_lib.render_mis(m, 2, 12)
+    assert_parity(got, ref, "bvh mis")
+    assert np.array_equal(got8, ref8)
