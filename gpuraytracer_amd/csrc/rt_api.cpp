@@ -52,6 +52,7 @@ struct rt_ctx {
     size_t out_cap = 0;     // bytes
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    uint32_t lanes = 0;  // RTPT_LANES=1|4|16: lanes per pixel (tuning knob; 0 = auto)
     rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|pairsmem|sorted|bvh (tuning knob)
     std::string err;
 };
@@ -227,6 +228,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.accumulate = p->accumulate ? 1u : 0u;
     K.samples_total = (uint32_t)total;
     K.flags = (p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u;
+    K.lanes = c->lanes;
     {
         const uint64_t imax = (uint64_t)c->seed_max + p->sample_base + (p->spp ? p->spp - 1u : 0u);
         K.max_index = imax > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)imax;
@@ -445,6 +447,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
     c->device = d->device;
+    if (const char* m = getenv("RTPT_LANES")) c->lanes = (uint32_t)atoi(m);
     if (const char* m = getenv("RTPT_SCENE_MEM")) {
         if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;

@@ -377,7 +377,12 @@ size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 #ifndef RT_MIN_WAVES_PER_EU_SPH
 #define RT_MIN_WAVES_PER_EU_SPH 8
 #endif
-template <int B, int GEO, bool SPH, bool SMALL>
+// L lanes per pixel (1, 4 or 16: more lanes when the launch has few pixels,
+// e.g. one GPU's share of a multi-GPU frame): lane `sub` of a pixel's
+// group traces samples n = r*L + sub of round r, and after every round the L
+// colours are shuffled within the wave and added to the pixel's sum in sample
+// order n — the same sequence of fp32 additions as one lane per pixel.
+template <int B, int GEO, bool SPH, bool SMALL, int L = 1>
 __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_MIN_WAVES_PER_EU) void path_trace_kernel(KParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
@@ -408,10 +413,14 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
     sv.nN = SPH ? P.nN : 0u;
     sv.sph_perm = P.sph_perm;
 
+    // wave = 64/L pixels: 8x8 (L=1), 4x4 (L=4), 2x2 (L=16), or one row of 64/L
+    // pixels for interleaved rows (launcher's wave_w); workgroup = 2x2 waves
+    const uint32_t kWX = (L == 1) ? 8u : P.wave_w, kWY = (64u / L) / kWX;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t j = blockIdx.y * kTile + (wave >> 1) * 8u + (lane >> 3);
-    if (x >= (uint32_t)P.W || j >= P.row_count) return;
+    const uint32_t pix = lane / L, sub = lane % L;
+    const uint32_t x = blockIdx.x * (2 * kWX) + (wave & 1u) * kWX + (pix % kWX);
+    const uint32_t j = blockIdx.y * (2 * kWY) + (wave >> 1) * kWY + (pix / kWX);
+    if (x >= (uint32_t)P.W || j >= P.row_count) return;  // a pixel's L lanes leave together
     const uint32_t y = P.row_start + j * P.row_step;
     const size_t o = (size_t)j * (size_t)P.W + x;
 
@@ -423,21 +432,36 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
     }
     const f3 cu = ld_f3(P.cam_u), cv = ld_f3(P.cam_v), cw = ld_f3(P.cam_w);
     const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
-    for (uint32_t n = 0; n < P.spp; ++n) {                       // :34
+    const uint32_t rounds = (P.spp + (L - 1)) / L;
+    for (uint32_t r = 0; r < rounds; ++r) {                      // :34
+        const uint32_t n = r * L + sub;
         PathState s;
-        s.i = seed + (P.sample_base + n);
-        const float jx = halton_dim<0, SMALL>(s.i), jy = halton_dim<1, SMALL>(s.i);   // :39-40
-        // generateCameraRay (sampling.metal:125-157)
-        const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
-        const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
-        const float sh = sx * P.halfW, th = ty * P.halfH;
-        s.d = normalize((cu * sh + cv * th) - cw);
-        s.o = ld_f3(P.cam_pos);
         s.acc = f3{0.0f, 0.0f, 0.0f};
-        s.thr = f3{1.0f, 1.0f, 1.0f};
-        trace_path<B, GEO, SPH, SMALL>(P, sv, s);                           // :47-102
-        lum = lum + s.acc;                                       // :103
+        if (L == 1 || n < P.spp) {
+            s.i = seed + (P.sample_base + n);
+            const float jx = halton_dim<0, SMALL>(s.i), jy = halton_dim<1, SMALL>(s.i);   // :39-40
+            // generateCameraRay (sampling.metal:125-157)
+            const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
+            const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
+            const float sh = sx * P.halfW, th = ty * P.halfH;
+            s.d = normalize((cu * sh + cv * th) - cw);
+            s.o = ld_f3(P.cam_pos);
+            s.thr = f3{1.0f, 1.0f, 1.0f};
+            trace_path<B, GEO, SPH, SMALL>(P, sv, s);                       // :47-102
+        }
+        if (L == 1) {
+            lum = lum + s.acc;                                   // :103
+        } else {
+            const int base = (int)(lane - sub);
+#pragma unroll
+            for (int k = 0; k < L; ++k) {                        // samples r*L + k, in order
+                const f3 c{__shfl(s.acc.x, base + k), __shfl(s.acc.y, base + k),
+                           __shfl(s.acc.z, base + k)};
+                if (r * L + (uint32_t)k < P.spp) lum = lum + c;  // :103
+            }
+        }
     }
+    if (L > 1 && sub != 0) return;                               // the group's sum is in every lane
     if (P.sum) P.sum[o] = make_float4(lum.x, lum.y, lum.z, (float)P.samples_total);
     if (P.out) {
         const float fs = (float)P.samples_total;                 // :106
@@ -545,8 +569,40 @@ __global__ void fill_seeds_kernel(uint32_t* seeds, uint64_t key, uint64_t n) {
 
 namespace {
 
+// Lanes per pixel (measured on one GPU's share of the N-GPU weak-scaling frame,
+// tools/bench_share.py): 4 for ~1 M pixels and more (also +6 % on the whole
+// 1080p frame: 4x4-pixel waves, more lanes in flight), 16 below that (one GPU's
+// share at N = 4 and 8), never more than spp.
+inline int lanes_per_pixel(const KParams& P) {
+    if (P.lanes == 1 || P.lanes == 4 || P.lanes == 16) return P.spp >= P.lanes ? (int)P.lanes : 1;
+    const uint64_t px = (uint64_t)P.W * P.row_count;
+    const int want = px >= 1000000ull ? 4 : 16;
+    if (P.spp >= (uint32_t)want) return want;
+    return P.spp >= 4 ? 4 : 1;
+}
+
+template <int B, int GEO, bool SPH, bool SMALL, int L>
+hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
+    KParams Q = P;
+    // wave tile: compact (4x4, 2x2) for whole frames; one row of 64/L pixels
+    // when the rows are interleaved (row_step > 1), which keeps a wave's camera
+    // rays adjacent in the image (N = 8 share: 10,822 -> 11,211 Msamples/s)
+    Q.wave_w = (P.row_step > 1) ? 64u / L : (L == 4 ? 4u : 2u);
+    const uint32_t TX = 2 * Q.wave_w, TY = 2 * ((64u / L) / Q.wave_w);
+    const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);
+    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL, L>), grid, dim3(kBlockThreads),
+                       (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,
+                       stream, Q);
+    return hipGetLastError();
+}
+
 template <int B, int GEO, bool SPH, bool SMALL>
 hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
+    if (SMALL) {
+        const int lpp = lanes_per_pixel(P);
+        if (lpp == 16) return launch_tl<B, GEO, SPH, SMALL, 16>(P, lds_bytes, stream);
+        if (lpp == 4) return launch_tl<B, GEO, SPH, SMALL, 4>(P, lds_bytes, stream);
+    }
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(kBlockThreads),
                        (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,

@@ -45,6 +45,8 @@ struct KParams {
     uint32_t samples_total;   // S of `luminance /= samples`
     uint32_t flags;
     uint32_t max_index;       // max Halton index seed+n of this launch (0xFFFFFFFF: unknown/wraps)
+    uint32_t lanes;           // lanes per pixel: 0 = auto, else 1, 4 or 16 (tuning knob)
+    uint32_t wave_w;          // pixels per wave row (set by the launcher)
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);

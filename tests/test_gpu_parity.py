@@ -310,3 +310,19 @@ def test_triangle_bvh_forced_on_cornell_and_mis(monkeypatch):
     ref, ref8 = oracle_lib.render_mis(m, 2, 12)
     assert_parity(got, ref, "bvh mis")
     assert np.array_equal(got8, ref8)
+
+
+@pytest.mark.parametrize("lanes", ["1", "4", "16", "auto"])
+def test_lanes_per_pixel_and_interleaved_rows_bit_exact(lanes, monkeypatch):
+    # 1, 4 or 16 lanes per pixel (samples shuffled back into sample order) and
+    # one-row wave tiles for interleaved rows all give the oracle's sums
+    if lanes != "auto":
+        monkeypatch.setenv("RTPT_LANES", lanes)
+    s = Scene.cornell_box(56, 40)
+    sd = seed_splitmix(56, 40)
+    with Renderer(s, seeds=sd) as r:
+        full = r.render(RenderParams(spp=19, bounces=3))
+        tile = r.render(RenderParams(spp=19, bounces=3, row_start=2, row_step=5))
+    ref = oracle_lib.render(s, sd, 19, 3)
+    assert_parity(full, ref, "lanes" + lanes)
+    assert_parity(tile, ref[2::5], "tile lanes" + lanes)
