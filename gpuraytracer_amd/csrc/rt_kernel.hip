@@ -241,7 +241,7 @@ struct FusedChain<B, B, GEO, SMALL> {
 #endif
 template <int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv, PathState& s) {
-    if (RT_FUSED && GEO == kGeoPairLds && !SPH && B > 1) {
+    if (RT_FUSED && geo_pairs(GEO) && !SPH && B > 1) {
         float t = 1000.0f;                                  // sampling.metal:155
         const int id = closest_hit<GEO, false, true, 0>(sv, s.o, s.d, 0.001f, &t);
         if (id >= 0) FusedChain<0, B, GEO, SMALL>::run(P, sv, s, id, t);
@@ -434,10 +434,12 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
     const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
     const uint32_t rounds = (P.spp + (L - 1)) / L;
     for (uint32_t r = 0; r < rounds; ++r) {                      // :34
-        const uint32_t n = r * L + sub;
+        // a lane past the last sample re-traces the last one (discarded below):
+        // no divergent branch around the path
+        const uint32_t n = (L == 1) ? r : min(r * L + sub, P.spp - 1u);
         PathState s;
         s.acc = f3{0.0f, 0.0f, 0.0f};
-        if (L == 1 || n < P.spp) {
+        {
             s.i = seed + (P.sample_base + n);
             const float jx = halton_dim<0, SMALL>(s.i), jy = halton_dim<1, SMALL>(s.i);   // :39-40
             // generateCameraRay (sampling.metal:125-157)
