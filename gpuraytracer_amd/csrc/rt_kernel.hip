@@ -430,6 +430,15 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
         const float4 prev = P.sum[o];
         lum = f3{prev.x, prev.y, prev.z};
     }
+    // L > 1: the pixel's running sum lives in LDS (its group leader adds to it),
+    // which keeps three VGPRs free across the path traversal
+    __shared__ float lum_s[L > 1 ? 3 * (kBlockThreads / L) : 1];
+    const uint32_t slot = threadIdx.x / L;
+    if (L > 1 && sub == 0) {
+        lum_s[3 * slot] = lum.x;
+        lum_s[3 * slot + 1] = lum.y;
+        lum_s[3 * slot + 2] = lum.z;
+    }
     const f3 cu = ld_f3(P.cam_u), cv = ld_f3(P.cam_v), cw = ld_f3(P.cam_w);
     const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
     const uint32_t rounds = (P.spp + (L - 1)) / L;
@@ -455,15 +464,26 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
             lum = lum + s.acc;                                   // :103
         } else {
             const int base = (int)(lane - sub);
+            f3 c[L];
 #pragma unroll
-            for (int k = 0; k < L; ++k) {                        // samples r*L + k, in order
-                const f3 c{__shfl(s.acc.x, base + k), __shfl(s.acc.y, base + k),
-                           __shfl(s.acc.z, base + k)};
-                if (r * L + (uint32_t)k < P.spp) lum = lum + c;  // :103
+            for (int k = 0; k < L; ++k)                          // samples r*L + k
+                c[k] = f3{__shfl(s.acc.x, base + k), __shfl(s.acc.y, base + k),
+                          __shfl(s.acc.z, base + k)};
+            if (sub == 0) {
+                f3 acc{lum_s[3 * slot], lum_s[3 * slot + 1], lum_s[3 * slot + 2]};
+#pragma unroll
+                for (int k = 0; k < L; ++k)                      // in sample order
+                    if (r * L + (uint32_t)k < P.spp) acc = acc + c[k];  // :103
+                lum_s[3 * slot] = acc.x;
+                lum_s[3 * slot + 1] = acc.y;
+                lum_s[3 * slot + 2] = acc.z;
             }
         }
     }
-    if (L > 1 && sub != 0) return;                               // the group's sum is in every lane
+    if (L > 1) {
+        if (sub != 0) return;
+        lum = f3{lum_s[3 * slot], lum_s[3 * slot + 1], lum_s[3 * slot + 2]};
+    }
     if (P.sum) P.sum[o] = make_float4(lum.x, lum.y, lum.z, (float)P.samples_total);
     if (P.out) {
         const float fs = (float)P.samples_total;                 // :106
