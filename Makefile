@@ -8,16 +8,20 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := gpuraytracer_amd
 SRC := $(PKG)/csrc
-BLD := build
+BLD ?= build
 COMMON := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude
 HOSTCXX ?= /opt/rocm/llvm/bin/clang++
-HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-slp-vectorize
+HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-slp-vectorize $(EXTRA)
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include
 
 OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
-HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp
+HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp $(SRC)/rt_halton.hpp
 
-all: $(PKG)/librtpt.so $(PKG)/rtrace oracle
+LIB ?= $(PKG)/librtpt.so
+
+all: $(LIB) $(PKG)/rtrace oracle
+
+lib: $(LIB)
 
 $(BLD):
 	mkdir -p $(BLD)
@@ -28,7 +32,7 @@ $(BLD)/%.o: $(SRC)/%.hip $(HDRS) $(SRC)/rt_trace.hpp | $(BLD)
 $(BLD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BLD)
 	$(HOSTCXX) $(HOSTFLAGS) -c $< -o $@
 
-$(PKG)/librtpt.so: $(OBJS)
+$(LIB): $(OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -Wl,--no-undefined
 
 $(PKG)/rtrace: $(SRC)/rtrace_main.cpp $(PKG)/librtpt.so $(HDRS)
@@ -41,4 +45,4 @@ clean:
 	rm -rf $(BLD) $(PKG)/librtpt.so $(PKG)/rtrace
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all lib oracle clean

@@ -260,11 +260,11 @@ def test_tonemap_matches_image_swift():
 
 
 def test_halton_small_magic_table():
-    """The kernel's 24-bit magic division (rt_kernel.hip kMagicM/kMagicS) is
+    """The kernel's 24-bit magic division (rt_halton.hpp kMagicM/kMagicS) is
     exact for every index < 2^21, for all 24 Halton bases."""
     import re
     src = open(os.path.join(os.path.dirname(GOLDEN), "..", "gpuraytracer_amd", "csrc",
-                            "rt_kernel.hip")).read()
+                            "rt_halton.hpp")).read()
     M = [int(v) for v in re.search(r"kMagicM\[24\] = \{([^}]*)\}", src).group(1).split(",")]
     S = [int(v) for v in re.search(r"kMagicS\[24\] = \{([^}]*)\}", src).group(1).split(",")]
     primes = [2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73,
