@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTPT_LIB overrides the in-tree library (A/B builds of the kernel).
 library_path = os.environ.get("RTPT_LIB") or os.path.join(_HERE, "librtpt.so")
@@ -87,7 +87,7 @@ class RenderParamsC(ctypes.Structure):  # rt_render_params
 class SceneInfo(ctypes.Structure):  # rt_scene_info
     _fields_ = [(n, ctypes.c_uint32) for n in
                 ("n_triangles", "n_triangle_pairs", "n_spheres", "lds_bytes",
-                 "n_sphere_nodes", "n_triangle_bvh_nodes")]
+                 "n_sphere_nodes", "n_triangle_bvh_nodes", "n_box_clusters", "pair_free_mask")]
 
 
 RT_OK = 0

@@ -28,6 +28,7 @@ struct rt_ctx {
     float4* d_tri_isect = nullptr;
     float4* d_tri_shade = nullptr;
     float4* d_pair_isect = nullptr;
+    float4* d_clusters = nullptr;
     float4* d_sph_isect = nullptr;
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
@@ -103,6 +104,7 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_tri_isect);
     (void)hipFree(c->d_tri_shade);
     (void)hipFree(c->d_pair_isect);
+    (void)hipFree(c->d_clusters);
     (void)hipFree(c->d_sph_isect);
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_sph_nodes);
@@ -194,6 +196,10 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.tri_isect = c->d_tri_isect;
     K.tri_shade = c->d_tri_shade;
     K.pair_isect = c->d_pair_isect;
+    K.clusters = c->d_clusters;
+    K.nC = (uint32_t)(c->scene.clusters.size() / 24);
+    K.pair_free = c->scene.pair_free_mask;
+    K.clu_w2 = c->scene.cluster_w2;
     K.sph_isect = c->d_sph_isect;
     K.sph_shade = c->d_sph_shade;
     K.sph_nodes = c->d_sph_nodes;
@@ -452,6 +458,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
         if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
         if (!strcmp(m, "sorted")) c->scene_mem = rt::SceneMem::kPairSorted;
+        if (!strcmp(m, "pairs")) c->scene_mem = rt::SceneMem::kPairLds;
         if (!strcmp(m, "pairsmem")) c->scene_mem = rt::SceneMem::kPairSmem;
         if (!strcmp(m, "bvh")) c->scene_mem = rt::SceneMem::kTriBvh;
     }
@@ -475,6 +482,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
         if ((e = upload(&c->d_tri_isect, s.tri_isect.data(), s.tri_isect.size() * sizeof(rt::TriIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_tri_shade, s.tri_shade.data(), s.tri_shade.size() * sizeof(rt::TriShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_pair_isect, s.pair_isect.data(), s.pair_isect.size() * sizeof(rt::PairIsect), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_clusters, s.clusters.data(), s.clusters.size() * sizeof(float), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_nodes, s.sph_nodes.data(), s.sph_nodes.size() * sizeof(rt::BvhNode), c->stream)) != hipSuccess ||
@@ -589,6 +597,8 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
         return fail(nullptr, RT_ERR_INVALID_ARG, err);
     info->n_triangles = (uint32_t)s.tri_isect.size();
     info->n_triangle_pairs = (uint32_t)s.pair_isect.size();
+    info->n_box_clusters = (uint32_t)(s.clusters.size() / 24);
+    info->pair_free_mask = s.pair_free_mask;
     info->n_spheres = (uint32_t)s.sph_isect.size();
     info->n_sphere_nodes = s.sph_layout_nodes;
     const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres,

@@ -312,12 +312,19 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
         sv.pair = P.pair_isect;
     } else if (GEO != kGeoTriGlobal) {
         // Stage the intersection records once per workgroup.
-        const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
-        const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
+        constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu;
+        const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
+        const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
+        if (GEO == kGeoPairClu)  // box clusters after the pair records
+            for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
+        sv.clu = lds + ng4;
+        sv.nC = P.nC;
+        sv.pair_free = P.pair_free;
+        sv.clu_w2 = P.clu_w2;
     } else {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
@@ -583,6 +590,7 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
     }
     switch (geo) {
         case kGeoPairLds: return launch_g<B, kGeoPairLds>(P, lds_bytes, stream);
+        case kGeoPairClu: return launch_g<B, kGeoPairClu>(P, lds_bytes, stream);
         case kGeoPairSmem: return launch_g<B, kGeoPairSmem>(P, lds_bytes, stream);
         case kGeoTriBvh: return launch_g<B, kGeoTriBvh>(P, lds_bytes, stream);
         case kGeoTriLds: return launch_g<B, kGeoTriLds>(P, lds_bytes, stream);
@@ -609,17 +617,24 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
     // triangle BVH whenever rt_create built one (kTriBvhMinTriangles or no LDS fit),
     // unless another layout is forced
     if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) geo = kGeoTriBvh;
+    // box clusters whenever rt_create found some
+    size_t lds_total = lds_bytes;
+    if (geo == kGeoPairLds && P.nC > 0 && mem == SceneMem::kAuto &&
+        lds_bytes + kCluF4 * P.nC * sizeof(float4) <= kMaxLdsBytes) {
+        geo = kGeoPairClu;
+        lds_total = lds_bytes + kCluF4 * P.nC * sizeof(float4);
+    }
     // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the
     // Cornell 1080p workload (barrier + occupancy cost).
     if (geo == kGeoPairLds && mem == SceneMem::kPairSorted &&
         lds_bytes + sorted_lds_extra_bytes() <= kMaxLdsBytes)
         geo = kGeoPairSorted;
     switch (bounces) {
-        case 0: return launch_b<0>(P, geo, lds_bytes, stream);
-        case 1: return launch_b<1>(P, geo, lds_bytes, stream);
-        case 2: return launch_b<2>(P, geo, lds_bytes, stream);
-        case 3: return launch_b<3>(P, geo, lds_bytes, stream);
-        case 4: return launch_b<4>(P, geo, lds_bytes, stream);
+        case 0: return launch_b<0>(P, geo, lds_total, stream);
+        case 1: return launch_b<1>(P, geo, lds_total, stream);
+        case 2: return launch_b<2>(P, geo, lds_total, stream);
+        case 3: return launch_b<3>(P, geo, lds_total, stream);
+        case 4: return launch_b<4>(P, geo, lds_total, stream);
         default: return hipErrorInvalidValue;
     }
 }

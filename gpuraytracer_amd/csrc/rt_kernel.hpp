@@ -14,6 +14,7 @@ constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
 constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
+constexpr uint32_t kCluF4 = 6;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
 constexpr uint32_t kTriBvhMinTriangles = 384;
@@ -47,11 +48,15 @@ struct KParams {
     uint32_t max_index;       // max Halton index seed+n of this launch (0xFFFFFFFF: unknown/wraps)
     uint32_t lanes;           // lanes per pixel: 0 = auto, else 1, 4 or 16 (tuning knob)
     uint32_t wave_w;          // pixels per wave row (set by the launcher)
+    const float4* clusters;   // box clusters, kCluF4 float4 each, or null
+    uint32_t nC;              // clusters (0: none)
+    uint32_t pair_free;       // pairs in no cluster (bit mask)
+    float clu_w2;             // 2 x face-plane tolerance of the clusters
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);
 // Where the workgroup reads the intersection records from.
-enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5 };
+enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5, kPairLds = 6 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
 hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
 // Arguments of the MIS integrator kernel (rt_mis.hip; Sources/gpuRaytracer/

@@ -428,6 +428,188 @@ static void build_pairs(CompiledScene* out, const rt_float3* verts, float margin
     out->pair_isect.swap(pairs);
 }
 
+// ---- box clusters ----------------------------------------
+// A run of consecutive pair records (quads) whose quads all lie on the faces of
+// one oriented box: the Cornell room (5 walls, open front), each rotated box
+// (6 faces), a lone rectangle (the light: a flat box).  The kernel slab-tests a
+// ray against the padded box and runs the exact pair test only on the faces
+// whose plane the ray can cross inside the box; an accepted hit point lies
+// within the culling margin of its quad, hence inside the padded box and within
+// the margin of its face plane, so no accepted triangle is skipped.
+namespace {
+struct D3 {
+    double x, y, z;
+};
+D3 d3(const rt_float3& v) { return D3{v.x, v.y, v.z}; }
+D3 sub(D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+double ddot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+D3 dcross(D3 a, D3 b) { return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+D3 dscale(D3 a, double s) { return D3{a.x * s, a.y * s, a.z * s}; }
+bool dnormalize(D3* a) {
+    const double l = sqrt(ddot(*a, *a));
+    if (!(l > 0.0) || !isfinite(l)) return false;
+    *a = dscale(*a, 1.0 / l);
+    return true;
+}
+
+struct BoxFit {
+    D3 u[3];
+    double lo[3], hi[3];
+    int slot_pair[6];
+};
+
+// Quads [k0, k1) of the pair list: do they lie on the faces of one box?
+bool fit_box(const rt_float3* verts, uint32_t k0, uint32_t k1, double tol, BoxFit* f) {
+    auto vtx = [&](uint32_t k, int i) { return d3(verts[6 * k + i]); };  // both triangles' corners
+    auto normal = [&](uint32_t k, D3* n) {
+        *n = dcross(sub(vtx(k, 1), vtx(k, 0)), sub(vtx(k, 2), vtx(k, 0)));
+        return dnormalize(n);
+    };
+    D3 n0;
+    if (!normal(k0, &n0)) return false;
+    f->u[0] = n0;
+    bool have1 = false;
+    for (uint32_t k = k0 + 1; k < k1 && !have1; ++k) {
+        D3 n;
+        if (!normal(k, &n)) return false;
+        const double c = ddot(n, n0);
+        if (fabs(c) > 1.0 - 1e-9) continue;
+        if (fabs(c) > 1e-6) return false;  // faces of a box are parallel or perpendicular
+        f->u[1] = sub(n, dscale(n0, c));
+        if (!dnormalize(&f->u[1])) return false;
+        have1 = true;
+    }
+    if (!have1) {  // flat (one plane): frame from the first quad's edge
+        D3 e = sub(vtx(k0, 1), vtx(k0, 0));
+        e = sub(e, dscale(n0, ddot(e, n0)));
+        if (!dnormalize(&e)) return false;
+        f->u[1] = e;
+    }
+    f->u[2] = dcross(f->u[0], f->u[1]);
+    if (!dnormalize(&f->u[2])) return false;
+    for (int a = 0; a < 3; ++a) {
+        f->lo[a] = INFINITY;
+        f->hi[a] = -INFINITY;
+    }
+    for (uint32_t k = k0; k < k1; ++k)
+        for (int i = 0; i < 6; ++i)
+            for (int a = 0; a < 3; ++a) {
+                const double p = ddot(f->u[a], vtx(k, i));
+                f->lo[a] = fmin(f->lo[a], p);
+                f->hi[a] = fmax(f->hi[a], p);
+            }
+    for (int s = 0; s < 6; ++s) f->slot_pair[s] = -1;
+    for (uint32_t k = k0; k < k1; ++k) {
+        D3 n;
+        if (!normal(k, &n)) return false;
+        int axis = -1;
+        for (int a = 0; a < 3; ++a)
+            if (fabs(ddot(n, f->u[a])) > 1.0 - 1e-9) axis = a;
+        if (axis < 0) return false;
+        // all four corners on the low or on the high face plane of that axis
+        int side = -1;
+        for (int sd = 0; sd < 2 && side < 0; ++sd) {
+            const double plane = sd ? f->hi[axis] : f->lo[axis];
+            bool on = true;
+            for (int i = 0; i < 6; ++i) on = on && fabs(ddot(f->u[axis], vtx(k, i)) - plane) <= tol;
+            if (on) side = sd;
+        }
+        if (side < 0) return false;
+        int slot = 2 * axis + side;
+        if (f->slot_pair[slot] >= 0) {
+            // a flat box has lo == hi: both slots name the same plane
+            if (f->hi[axis] - f->lo[axis] <= tol && f->slot_pair[slot ^ 1] < 0) slot ^= 1;
+            else return false;
+        }
+        f->slot_pair[slot] = (int)k;
+    }
+    return true;
+}
+}  // namespace
+
+static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t n_tri,
+                           float margin) {
+    out->clusters.clear();
+    out->pair_free_mask = 0;
+    out->cluster_w2 = 0.0f;
+    const uint32_t np = (uint32_t)out->pair_isect.size();
+    if (np == 0 || np > 31) return;
+    double ext = 0.0;
+    for (uint32_t k = 0; k < 3 * n_tri; ++k)
+        ext = fmax(ext, fmax(fabs(verts[k].x), fmax(fabs(verts[k].y), fabs(verts[k].z))));
+    // corners must sit on their face plane within tol (fp32 vertices of a
+    // rotated box are planar to ~1e-7 of the scene scale)
+    const double tol = 1e-5 * fmax(1.0, ext);
+    const double pad = (double)margin + tol;
+    uint32_t free_mask = 0;
+    std::vector<float> cl;
+    for (uint32_t k0 = 0; k0 < np;) {
+        BoxFit best, f;
+        uint32_t k1 = k0;
+        while (k1 < np && fit_box(verts, k0, k1 + 1, tol, &f)) {
+            best = f;
+            ++k1;
+        }
+        if (k1 == k0) {  // this quad is not a rectangle face of any box
+            free_mask |= 1u << k0;
+            ++k0;
+            continue;
+        }
+        // axis-aligned box: reorder to (+x, +y, +z) so the kernel can use the
+        // ray's own reciprocals (flag bit 0)
+        bool aligned = true;
+        int perm[3];
+        double sgn[3];
+        for (int a = 0; a < 3; ++a) {
+            const double c[3] = {best.u[a].x, best.u[a].y, best.u[a].z};
+            perm[a] = -1;
+            for (int j = 0; j < 3; ++j)
+                if (fabs(fabs(c[j]) - 1.0) == 0.0) {
+                    perm[a] = j;
+                    sgn[a] = c[j];
+                }
+            aligned = aligned && perm[a] >= 0;
+        }
+        if (aligned && perm[0] != perm[1] && perm[1] != perm[2] && perm[0] != perm[2]) {
+            BoxFit al = best;
+            for (int a = 0; a < 3; ++a) {
+                const int j = perm[a];
+                al.u[j] = D3{j == 0 ? 1.0 : 0.0, j == 1 ? 1.0 : 0.0, j == 2 ? 1.0 : 0.0};
+                al.lo[j] = sgn[a] > 0 ? best.lo[a] : -best.hi[a];
+                al.hi[j] = sgn[a] > 0 ? best.hi[a] : -best.lo[a];
+                al.slot_pair[2 * j] = best.slot_pair[2 * a + (sgn[a] > 0 ? 0 : 1)];
+                al.slot_pair[2 * j + 1] = best.slot_pair[2 * a + (sgn[a] > 0 ? 1 : 0)];
+            }
+            best = al;
+        } else {
+            aligned = false;
+        }
+        auto bits = [](uint32_t v) {
+            float f;
+            memcpy(&f, &v, 4);
+            return f;
+        };
+        for (int a = 0; a < 3; ++a) {
+            cl.push_back((float)best.u[a].x);
+            cl.push_back((float)best.u[a].y);
+            cl.push_back((float)best.u[a].z);
+            cl.push_back((float)(best.lo[a] - pad));
+        }
+        cl.push_back((float)(best.hi[0] + pad));
+        cl.push_back((float)(best.hi[1] + pad));
+        cl.push_back((float)(best.hi[2] + pad));
+        cl.push_back(bits(aligned ? 1u : 0u));
+        for (int sl = 0; sl < 6; ++sl)  // pair bit of each face slot (2*axis + side)
+            cl.push_back(bits(best.slot_pair[sl] < 0 ? 0u : 1u << best.slot_pair[sl]));
+        cl.push_back(0.0f);
+        cl.push_back(0.0f);
+        k0 = k1;
+    }
+    out->clusters.swap(cl);
+    out->pair_free_mask = free_mask;
+    out->cluster_w2 = (float)(2.0 * pad);
+}
+
 static bool finite3(const rt_float3& v) {
     return isfinite(v.x) && isfinite(v.y) && isfinite(v.z);
 }
@@ -504,6 +686,7 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                                4e-5f * fmaxf(fabsf(cam.position.x),
                                              fmaxf(fabsf(cam.position.y), fabsf(cam.position.z))));
     build_pairs(out, verts, margin);
+    build_clusters(out, verts, n_tri, margin);
     out->margin = margin;
     for (int a = 0; a < 3; ++a) {
         out->tri_lo[a] = INFINITY;

@@ -135,6 +135,7 @@ enum Geo : int {
     kGeoPairSmem = 4,   // shared-edge pair records read with scalar loads (no LDS)
     kGeoTriBvh = 5,     // GPU-built triangle BVH (rt_lbvh.hip), records from global
     kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
+    kGeoPairClu = 6,    // pair records in LDS + box clusters
 };
 
 constexpr bool geo_pairs(int g) { return g == kGeoPairLds || g == kGeoPairSmem; }
@@ -150,6 +151,10 @@ struct SceneView {
     const uint32_t* tperm;    // leaf order -> triangle id
     uint32_t nTN;
     uint32_t nT, nP, nS, nN;
+    const float4* clu;        // box clusters, 4 float4 each (kGeoPairClu)
+    uint32_t nC;
+    uint32_t pair_free;       // pairs in no cluster: tested by every lane
+    float clu_w2;             // 2 x face-plane tolerance
 };
 
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
@@ -374,6 +379,119 @@ __device__ __forceinline__ bool tri_bvh_any(const float4* __restrict__ node,
     return found;
 }
 
+// ---- box clusters ------------------------------------------
+// Candidate pairs of one ray among the clustered pairs: bit k set when pair k
+// can hold an accepted hit with t in (tmin, tmax).  Per cluster: slab test of
+// the padded box along its three axes ([Tlo, Thi], widened by a relative
+// slack for the approximate rcp arithmetic), then a face is a candidate when
+// its plane's interval [t_plane -/+ w] meets [Tlo, Thi] — in a box that is the
+// face the ray enters through and the one it leaves through (two or three more
+// near an edge or corner).  Only speed depends on the rounding here.
+__device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o, f3 d, float tmin,
+                                                       float tmax) {
+    constexpr float kEps = 1.52587890625e-05f;  // 2^-16 relative slack
+    // per-ray terms of the axis-aligned clusters (flag bit 0): t = lo * invd - o * invd
+    const RayBox rb = ray_box(o, d);
+    uint32_t mask = 0;
+    for (uint32_t c = 0; c < sv.nC; ++c) {
+        const float4* r = sv.clu + kCluF4 * c;
+        const float4 H = r[3], M0 = r[4], M1 = r[5];
+        float en[3], ex[3], ida[3];
+        if (__float_as_uint(H.w) & 1u) {
+            const float4 A0 = r[0], A1 = r[1], A2 = r[2];
+            const float lo[3] = {A0.w, A1.w, A2.w}, hi[3] = {H.x, H.y, H.z};
+            const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
+            const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float t0 = fmaf(lo[a], iv[a], -oi[a]), t1 = fmaf(hi[a], iv[a], -oi[a]);
+                en[a] = fminf(t0, t1);
+                ex[a] = fmaxf(t0, t1);
+                ida[a] = iv[a];
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float4 A = r[a];
+                const float hi = a == 0 ? H.x : (a == 1 ? H.y : H.z);
+                const float oa = dot(f3{A.x, A.y, A.z}, o), da = dot(f3{A.x, A.y, A.z}, d);
+                ida[a] = safe_rcp(da);
+                const float t0 = (A.w - oa) * ida[a], t1 = (hi - oa) * ida[a];
+                en[a] = fminf(t0, t1);
+                ex[a] = fmaxf(t0, t1);
+            }
+        }
+        const float tlo0 = fmaxf(fmaxf(en[0], en[1]), fmaxf(en[2], tmin));
+        const float thi0 = fminf(fminf(ex[0], ex[1]), fminf(ex[2], tmax));
+        const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
+        const uint32_t m[6] = {__float_as_uint(M0.x), __float_as_uint(M0.y), __float_as_uint(M0.z),
+                               __float_as_uint(M0.w), __float_as_uint(M1.x), __float_as_uint(M1.y)};
+        uint32_t cm = 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            // a ray with d_a >= 0 enters through the low face (slot 2a) and
+            // leaves through the high one (2a + 1)
+            const bool neg = ida[a] < 0.0f;
+            const uint32_t m_en = neg ? m[2 * a + 1] : m[2 * a], m_ex = neg ? m[2 * a] : m[2 * a + 1];
+            const float w = fmaf(fabsf(en[a]), kEps, sv.clu_w2 * fabsf(ida[a]));
+            const float wx = fmaf(fabsf(ex[a]), kEps, sv.clu_w2 * fabsf(ida[a]));
+            cm |= (en[a] + w >= tlo) ? m_en : 0u;
+            cm |= (ex[a] - wx <= thi) ? m_ex : 0u;
+        }
+        mask |= (tlo <= thi) ? cm : 0u;
+    }
+    return mask;
+}
+
+// Exact pair test (the same arithmetic as the brute-force loops) with the
+// hit ranked lexicographically by (t, triangle id): pairs are visited out of
+// id order here, and (t, id) order is what the id-ordered scan with strict
+// '<' computes.  ANY = shadow any-hit: *id becomes >= 0 on any accepted hit.
+template <bool ANY>
+__device__ __forceinline__ void pair_test_rank(const float4* r, uint32_t k, f3 o, f3 d, float tmin,
+                                               float* best, int* id) {
+    const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+    const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
+    const bool pa = bary_ok(q.denA, q.a1, q.a2);
+    const bool pb = bary_ok(q.denB, q.b1, q.b2);
+    if (pa || pb) {
+        const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+        const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
+        const int ia = (int)(pa ? 2 * k : 2 * k + 1);
+        if (t > tmin && (t < *best || (!ANY && t == *best && ia < *id))) {
+            if (!ANY) *best = t;
+            *id = ia;
+        }
+        if (pa && pb) {
+            const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
+            const int ib = (int)(2 * k + 1);
+            if (t2 > tmin && (t2 < *best || (!ANY && t2 == *best && ib < *id))) {
+                if (!ANY) *best = t2;
+                *id = ib;
+            }
+        }
+    }
+}
+
+// Closest hit / any hit over the pair records with box clusters: the
+// unclustered pairs by every lane (wave-uniform records, LDS broadcast), then
+// each lane's own candidate pairs (per-lane LDS reads).  For ANY, *best is
+// tmax and is not changed.
+template <bool ANY>
+__device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, float tmin,
+                                              float* best, int* id) {
+    for (uint32_t free = sv.pair_free; free != 0u; free &= free - 1u) {
+        const uint32_t k = (uint32_t)__builtin_ctz(free);
+        pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);
+    }
+    uint32_t cand = cluster_candidates(sv, o, d, tmin, *best);
+    while (cand != 0u && !(ANY && *id >= 0)) {
+        const uint32_t k = (uint32_t)__builtin_ctz(cand);
+        cand &= cand - 1u;
+        pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);
+    }
+}
+
 // closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
 // Primitives are tested in id order; a strictly smaller t wins (ties keep the
 // lower id), exactly as the oracle.
@@ -385,7 +503,9 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
                                            float* t_io) {
     float best = *t_io;
     int id = -1;
-    if (geo_pairs(GEO)) {
+    if (GEO == kGeoPairClu) {
+        cluster_query<false>(sv, o, d, tmin, &best, &id);
+    } else if (geo_pairs(GEO)) {
         f3 seg_lo, seg_hi;
         if (CULL) {
             const f3 e = o + d * best;
@@ -456,7 +576,12 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
 template <int GEO, bool SPH, bool PACKET>
 __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
                                         f3 seg_lo, f3 seg_hi) {
-    if (geo_pairs(GEO)) {
+    if (GEO == kGeoPairClu) {
+        float tm = tmax;
+        int id = -1;
+        cluster_query<true>(sv, o, d, tmin, &tm, &id);
+        if (id >= 0) return true;
+    } else if (geo_pairs(GEO)) {
         for (uint32_t k = 0; k < sv.nP; ++k) {
             const float4* r = sv.pair + kPairF4 * k;
             const float4 b0 = r[5], b1 = r[6];

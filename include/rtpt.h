@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RTPT_ABI_VERSION 2
+#define RTPT_ABI_VERSION 3
 
 /* Maximum bounce count: Halton dimensions 2+5b..5+5b must stay inside the
  * 24-entry `primes[]` table (`RTrace/sampling.metal:97-104`); b <= 3. */
@@ -185,6 +185,8 @@ typedef struct rt_scene_info {
     uint32_t lds_bytes;          /* intersection records staged per workgroup (0: read from global) */
     uint32_t n_sphere_nodes;     /* sphere BVH nodes per layout (32 B each, 8 layouts, global) */
     uint32_t n_triangle_bvh_nodes; /* GPU-built triangle BVH nodes per layout (0: LDS layouts) */
+    uint32_t n_box_clusters;     /* pair runs on the faces of one oriented box (slab-tested first) */
+    uint32_t pair_free_mask;     /* pairs in no box cluster (bit k = pair k) */
 } rt_scene_info;
 int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
 
