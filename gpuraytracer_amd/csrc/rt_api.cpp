@@ -197,9 +197,8 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.tri_shade = c->d_tri_shade;
     K.pair_isect = c->d_pair_isect;
     K.clusters = c->d_clusters;
-    K.nC = (uint32_t)(c->scene.clusters.size() / 24);
+    K.nC = (uint32_t)(c->scene.clusters.size() / (4 * rt::kCluF4));
     K.pair_free = c->scene.pair_free_mask;
-    K.clu_w2 = c->scene.cluster_w2;
     K.sph_isect = c->d_sph_isect;
     K.sph_shade = c->d_sph_shade;
     K.sph_nodes = c->d_sph_nodes;
@@ -597,7 +596,7 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
         return fail(nullptr, RT_ERR_INVALID_ARG, err);
     info->n_triangles = (uint32_t)s.tri_isect.size();
     info->n_triangle_pairs = (uint32_t)s.pair_isect.size();
-    info->n_box_clusters = (uint32_t)(s.clusters.size() / 24);
+    info->n_box_clusters = (uint32_t)(s.clusters.size() / (4 * rt::kCluF4));
     info->pair_free_mask = s.pair_free_mask;
     info->n_spheres = (uint32_t)s.sph_isect.size();
     info->n_sphere_nodes = s.sph_layout_nodes;
@@ -607,7 +606,10 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     const bool bvh = info->n_triangles > rt::kTriBvhMinTriangles ||
                      std::min(lds, lds_single) > rt::kMaxLdsBytes;
     info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
-    info->lds_bytes = (!bvh && lds <= rt::kMaxLdsBytes) ? (uint32_t)lds : 0u;
+    const size_t lds_clu = lds + rt::kCluF4 * sizeof(float) * 4 * info->n_box_clusters;
+    info->lds_bytes = (!bvh && lds <= rt::kMaxLdsBytes)
+                          ? (uint32_t)(lds_clu <= rt::kMaxLdsBytes ? lds_clu : lds)
+                          : 0u;
     return RT_OK;
 }
 

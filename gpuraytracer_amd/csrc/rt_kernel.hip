@@ -324,7 +324,6 @@ __global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_M
         sv.clu = lds + ng4;
         sv.nC = P.nC;
         sv.pair_free = P.pair_free;
-        sv.clu_w2 = P.clu_w2;
     } else {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;

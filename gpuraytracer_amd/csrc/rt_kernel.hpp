@@ -14,7 +14,7 @@ constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
 constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
-constexpr uint32_t kCluF4 = 6;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
+constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
 constexpr uint32_t kTriBvhMinTriangles = 384;
@@ -51,7 +51,6 @@ struct KParams {
     const float4* clusters;   // box clusters, kCluF4 float4 each, or null
     uint32_t nC;              // clusters (0: none)
     uint32_t pair_free;       // pairs in no cluster (bit mask)
-    float clu_w2;             // 2 x face-plane tolerance of the clusters
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);

@@ -528,10 +528,9 @@ bool fit_box(const rt_float3* verts, uint32_t k0, uint32_t k1, double tol, BoxFi
 }  // namespace
 
 static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t n_tri,
-                           float margin) {
+                           float margin, double cam_ext) {
     out->clusters.clear();
     out->pair_free_mask = 0;
-    out->cluster_w2 = 0.0f;
     const uint32_t np = (uint32_t)out->pair_isect.size();
     if (np == 0 || np > 31) return;
     double ext = 0.0;
@@ -540,7 +539,10 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
     // corners must sit on their face plane within tol (fp32 vertices of a
     // rotated box are planar to ~1e-7 of the scene scale)
     const double tol = 1e-5 * fmax(1.0, ext);
-    const double pad = (double)margin + tol;
+    // Along a face's normal an accepted hit point is off the face plane only by
+    // the rounding of t (~1e-7 of the distance travelled) and the planarity
+    // tol; across a face it can be off by the bary rounding: the culling margin.
+    const double tol_n = tol + 1e-5 * fmax(ext, cam_ext);
     uint32_t free_mask = 0;
     std::vector<float> cl;
     for (uint32_t k0 = 0; k0 < np;) {
@@ -555,34 +557,49 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
             ++k0;
             continue;
         }
-        // axis-aligned box: reorder to (+x, +y, +z) so the kernel can use the
-        // ray's own reciprocals (flag bit 0)
-        bool aligned = true;
-        int perm[3];
-        double sgn[3];
+        // Axes that are world axes move to that position with a + sign, so the
+        // kernel reuses the ray's own reciprocals for them (flags bit a).
+        {
+            BoxFit cf = best;
+            int pos[3] = {-1, -1, -1};
+            bool used[3] = {false, false, false};
+            for (int a = 0; a < 3; ++a) {
+                const double c[3] = {best.u[a].x, best.u[a].y, best.u[a].z};
+                for (int j = 0; j < 3; ++j)
+                    if (fabs(c[j]) == 1.0 && !used[j]) {
+                        pos[a] = j;
+                        used[j] = true;
+                    }
+            }
+            for (int a = 0; a < 3; ++a)
+                for (int j = 0; j < 3 && pos[a] < 0; ++j)
+                    if (!used[j]) {
+                        pos[a] = j;
+                        used[j] = true;
+                    }
+            for (int a = 0; a < 3; ++a) {
+                const int j = pos[a];
+                const double c[3] = {best.u[a].x, best.u[a].y, best.u[a].z};
+                const bool flip = c[j] == -1.0;
+                cf.u[j] = flip ? dscale(best.u[a], -1.0) : best.u[a];
+                cf.lo[j] = flip ? -best.hi[a] : best.lo[a];
+                cf.hi[j] = flip ? -best.lo[a] : best.hi[a];
+                cf.slot_pair[2 * j] = best.slot_pair[2 * a + (flip ? 1 : 0)];
+                cf.slot_pair[2 * j + 1] = best.slot_pair[2 * a + (flip ? 0 : 1)];
+            }
+            best = cf;
+        }
+        uint32_t flags = 0;
         for (int a = 0; a < 3; ++a) {
             const double c[3] = {best.u[a].x, best.u[a].y, best.u[a].z};
-            perm[a] = -1;
-            for (int j = 0; j < 3; ++j)
-                if (fabs(fabs(c[j]) - 1.0) == 0.0) {
-                    perm[a] = j;
-                    sgn[a] = c[j];
-                }
-            aligned = aligned && perm[a] >= 0;
+            if (c[a] == 1.0) flags |= 1u << a;
         }
-        if (aligned && perm[0] != perm[1] && perm[1] != perm[2] && perm[0] != perm[2]) {
-            BoxFit al = best;
-            for (int a = 0; a < 3; ++a) {
-                const int j = perm[a];
-                al.u[j] = D3{j == 0 ? 1.0 : 0.0, j == 1 ? 1.0 : 0.0, j == 2 ? 1.0 : 0.0};
-                al.lo[j] = sgn[a] > 0 ? best.lo[a] : -best.hi[a];
-                al.hi[j] = sgn[a] > 0 ? best.hi[a] : -best.lo[a];
-                al.slot_pair[2 * j] = best.slot_pair[2 * a + (sgn[a] > 0 ? 0 : 1)];
-                al.slot_pair[2 * j + 1] = best.slot_pair[2 * a + (sgn[a] > 0 ? 1 : 0)];
-            }
-            best = al;
-        } else {
-            aligned = false;
+        // padding per axis: tol_n, plus the margin if some face lies across it
+        double pad[3];
+        for (int a = 0; a < 3; ++a) {
+            bool across = false;
+            for (int sl = 0; sl < 6; ++sl) across = across || (best.slot_pair[sl] >= 0 && sl / 2 != a);
+            pad[a] = tol_n + (across ? (double)margin : 0.0);
         }
         auto bits = [](uint32_t v) {
             float f;
@@ -593,21 +610,24 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
             cl.push_back((float)best.u[a].x);
             cl.push_back((float)best.u[a].y);
             cl.push_back((float)best.u[a].z);
-            cl.push_back((float)(best.lo[a] - pad));
+            cl.push_back((float)(best.lo[a] - pad[a]));
         }
-        cl.push_back((float)(best.hi[0] + pad));
-        cl.push_back((float)(best.hi[1] + pad));
-        cl.push_back((float)(best.hi[2] + pad));
-        cl.push_back(bits(aligned ? 1u : 0u));
+        cl.push_back((float)(best.hi[0] + pad[0]));
+        cl.push_back((float)(best.hi[1] + pad[1]));
+        cl.push_back((float)(best.hi[2] + pad[2]));
+        cl.push_back(bits(flags));
         for (int sl = 0; sl < 6; ++sl)  // pair bit of each face slot (2*axis + side)
             cl.push_back(bits(best.slot_pair[sl] < 0 ? 0u : 1u << best.slot_pair[sl]));
         cl.push_back(0.0f);
+        cl.push_back(0.0f);
+        // face-plane half width factor per axis: the face plane lies pad inside
+        // the padded slab, an accepted hit within tol_n of it
+        for (int a = 0; a < 3; ++a) cl.push_back((float)(pad[a] + tol_n));
         cl.push_back(0.0f);
         k0 = k1;
     }
     out->clusters.swap(cl);
     out->pair_free_mask = free_mask;
-    out->cluster_w2 = (float)(2.0 * pad);
 }
 
 static bool finite3(const rt_float3& v) {
@@ -686,7 +706,8 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
                                4e-5f * fmaxf(fabsf(cam.position.x),
                                              fmaxf(fabsf(cam.position.y), fabsf(cam.position.z))));
     build_pairs(out, verts, margin);
-    build_clusters(out, verts, n_tri, margin);
+    build_clusters(out, verts, n_tri, margin,
+                   fmax(fabs(cam.position.x), fmax(fabs(cam.position.y), fabs(cam.position.z))));
     out->margin = margin;
     for (int a = 0; a < 3; ++a) {
         out->tri_lo[a] = INFINITY;

@@ -97,14 +97,14 @@ struct CompiledScene {
     std::vector<BvhNode> sph_nodes;     // 8 octant layouts of sph_layout_nodes nodes each
     uint32_t sph_layout_nodes = 0;
     std::vector<SphShade> sph_shade;    // by sphere id
-    // Box clusters over the pair records: 24 floats each,
+    // Box clusters over the pair records: 28 floats each,
     // (u0.xyz, lo0) (u1.xyz, lo1) (u2.xyz, lo2) (hi0, hi1, hi2, flags)
-    // (m0, m1, m2, m3) (m4, m5, 0, 0): an oriented box (padded extents) whose
-    // faces hold consecutive pair records; m_s = bit of the pair on face slot
-    // s = 2*axis + side (0: none); flags bit 0 = axes are +x, +y, +z.
+    // (m0, m1, m2, m3) (m4, m5, 0, 0) (w0, w1, w2, 0): an oriented box (padded
+    // extents) whose faces hold consecutive pair records; m_s = bit of the pair
+    // on face slot s = 2*axis + side (0: none); flags bit a = axis a is world
+    // axis a (+); w_a = face-plane half width factor of axis a.
     std::vector<float> clusters;
     uint32_t pair_free_mask = 0;        // pairs in no cluster (tested by every lane)
-    float cluster_w2 = 0.0f;            // 2 x the face-plane tolerance
     float tri_lo[3], tri_hi[3];         // bounds of the triangle vertices (BVH build)
     float margin = 0.0f;                // culling margin
     MisLightConst mis_light;

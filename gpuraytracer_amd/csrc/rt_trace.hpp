@@ -117,6 +117,8 @@ __device__ __forceinline__ bool sph_test(const float4& S, f3 o, f3 d, float a, f
 // Slot groups of 4 per query kind q (0: camera closest hit, 1: bounce closest
 // hit, 2: shadow any-hit): [4q] pair records visited per wave, [4q+1] records
 // tested, [4q+2] active lanes summed over tested records, [4q+3] division blocks.
+// Box-cluster queries: [12] queries per wave, [13] candidate rounds per wave,
+// [14] lanes summed over rounds, [15] lanes summed over queries.
 #ifdef RT_STATS
 __device__ unsigned long long g_rt_stats[16];
 __device__ __forceinline__ void stat_wave(int slot, unsigned long long v) {
@@ -154,7 +156,6 @@ struct SceneView {
     const float4* clu;        // box clusters, 4 float4 each (kGeoPairClu)
     uint32_t nC;
     uint32_t pair_free;       // pairs in no cluster: tested by every lane
-    float clu_w2;             // 2 x face-plane tolerance
 };
 
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
@@ -390,36 +391,33 @@ __device__ __forceinline__ bool tri_bvh_any(const float4* __restrict__ node,
 __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o, f3 d, float tmin,
                                                        float tmax) {
     constexpr float kEps = 1.52587890625e-05f;  // 2^-16 relative slack
-    // per-ray terms of the axis-aligned clusters (flag bit 0): t = lo * invd - o * invd
+    // per-ray terms of world-aligned box axes: t = lo * invd - o * invd
     const RayBox rb = ray_box(o, d);
+    const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
+    const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
     uint32_t mask = 0;
     for (uint32_t c = 0; c < sv.nC; ++c) {
         const float4* r = sv.clu + kCluF4 * c;
-        const float4 H = r[3], M0 = r[4], M1 = r[5];
+        const float4 H = r[3], M0 = r[4], M1 = r[5], W = r[6];
+        const uint32_t flags = __float_as_uint(H.w);
+        const float hi[3] = {H.x, H.y, H.z}, wf[3] = {W.x, W.y, W.z};
         float en[3], ex[3], ida[3];
-        if (__float_as_uint(H.w) & 1u) {
-            const float4 A0 = r[0], A1 = r[1], A2 = r[2];
-            const float lo[3] = {A0.w, A1.w, A2.w}, hi[3] = {H.x, H.y, H.z};
-            const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
-            const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const float t0 = fmaf(lo[a], iv[a], -oi[a]), t1 = fmaf(hi[a], iv[a], -oi[a]);
-                en[a] = fminf(t0, t1);
-                ex[a] = fmaxf(t0, t1);
+        for (int a = 0; a < 3; ++a) {
+            const float4 A = r[a];
+            float t0, t1;
+            if (flags & (1u << a)) {  // wave-uniform
                 ida[a] = iv[a];
-            }
-        } else {
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const float4 A = r[a];
-                const float hi = a == 0 ? H.x : (a == 1 ? H.y : H.z);
+                t0 = fmaf(A.w, iv[a], -oi[a]);
+                t1 = fmaf(hi[a], iv[a], -oi[a]);
+            } else {
                 const float oa = dot(f3{A.x, A.y, A.z}, o), da = dot(f3{A.x, A.y, A.z}, d);
                 ida[a] = safe_rcp(da);
-                const float t0 = (A.w - oa) * ida[a], t1 = (hi - oa) * ida[a];
-                en[a] = fminf(t0, t1);
-                ex[a] = fmaxf(t0, t1);
+                t0 = (A.w - oa) * ida[a];
+                t1 = (hi[a] - oa) * ida[a];
             }
+            en[a] = fminf(t0, t1);
+            ex[a] = fmaxf(t0, t1);
         }
         const float tlo0 = fmaxf(fmaxf(en[0], en[1]), fmaxf(en[2], tmin));
         const float thi0 = fminf(fminf(ex[0], ex[1]), fminf(ex[2], tmax));
@@ -430,13 +428,13 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             // a ray with d_a >= 0 enters through the low face (slot 2a) and
-            // leaves through the high one (2a + 1)
+            // leaves through the high one (2a + 1); the face plane lies
+            // wf * |1/d_a| inside the padded slab, +- the tolerance
             const bool neg = ida[a] < 0.0f;
             const uint32_t m_en = neg ? m[2 * a + 1] : m[2 * a], m_ex = neg ? m[2 * a] : m[2 * a + 1];
-            const float w = fmaf(fabsf(en[a]), kEps, sv.clu_w2 * fabsf(ida[a]));
-            const float wx = fmaf(fabsf(ex[a]), kEps, sv.clu_w2 * fabsf(ida[a]));
-            cm |= (en[a] + w >= tlo) ? m_en : 0u;
-            cm |= (ex[a] - wx <= thi) ? m_ex : 0u;
+            const float wa = wf[a] * fabsf(ida[a]);
+            cm |= (en[a] + fmaf(fabsf(en[a]), kEps, wa) >= tlo) ? m_en : 0u;
+            cm |= (ex[a] - fmaf(fabsf(ex[a]), kEps, wa) <= thi) ? m_ex : 0u;
         }
         mask |= (tlo <= thi) ? cm : 0u;
     }
@@ -485,7 +483,11 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
         pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);
     }
     uint32_t cand = cluster_candidates(sv, o, d, tmin, *best);
+    RT_STAT(12, 1);
+    RT_STAT(15, __popcll(__ballot(1)));
     while (cand != 0u && !(ANY && *id >= 0)) {
+        RT_STAT(13, 1);
+        RT_STAT(14, __popcll(__ballot(1)));
         const uint32_t k = (uint32_t)__builtin_ctz(cand);
         cand &= cand - 1u;
         pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);

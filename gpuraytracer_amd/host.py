@@ -138,6 +138,42 @@ class Scene:
         mm[36:, 5] = 0.5
         return cls(base.camera, mats, verts, base.light)
 
+    @classmethod
+    def random_boxes(cls, width: int = 1920, height: int = 1080, n_boxes: int = 4,
+                     seed: int = 3) -> "Scene":
+        """Box-cluster stress scene: the Cornell room (walls = ids 0-9) plus
+        ``n_boxes`` randomly rotated boxes (12 triangles each, one shared-edge
+        pair per face) and the light rectangle last (numpy PCG64 ``seed``)."""
+        base = cls.cornell_box(width, height)
+        rng = np.random.default_rng(seed)
+        n = 10 + 12 * n_boxes + 2
+        mats = (MaterialGPU * n)()
+        verts = (float3 * (3 * n))()
+        ctypes.memmove(ctypes.addressof(mats), ctypes.addressof(base.materials), 10 * 48)
+        ctypes.memmove(ctypes.addressof(verts), ctypes.addressof(base.vertices), 30 * 16)
+        vv = np.frombuffer(verts, np.float32).reshape(-1, 4)
+        mm = np.frombuffer(mats, np.float32).reshape(-1, 12)
+        for b in range(n_boxes):
+            c = rng.uniform(-1.8, 1.8, 3)
+            h = rng.uniform(0.15, 0.7, 3)
+            R, _ = np.linalg.qr(rng.normal(size=(3, 3)))
+            col = rng.uniform(0.1, 0.9, 3)
+            for f in range(6):
+                a, s = f // 2, (1.0 if f % 2 else -1.0)
+                i, j = (a + 1) % 3, (a + 2) % 3
+                P = [c + s * h[a] * R[a] + u * h[i] * R[i] + v * h[j] * R[j]
+                     for u, v in ((-1, -1), (1, -1), (1, 1), (-1, 1))]
+                for t, tri in enumerate(((P[0], P[1], P[2]), (P[0], P[2], P[3]))):
+                    k = 10 + 12 * b + 2 * f + t
+                    vv[3 * k:3 * k + 3, :3] = np.array(tri, np.float32)
+                    mm[k, 0:3] = col
+                    mm[k, 3] = 1.0
+                    mm[k, 5] = 0.5
+        ctypes.memmove(ctypes.addressof(mats) + (n - 2) * 48, ctypes.addressof(base.materials) + 34 * 48, 96)
+        ctypes.memmove(ctypes.addressof(verts) + 3 * (n - 2) * 16,
+                       ctypes.addressof(base.vertices) + 3 * 34 * 16, 96)
+        return cls(base.camera, mats, verts, base.light)
+
     def describe(self) -> dict:
         """Device layout rt_create would choose (rt_scene_describe)."""
         info = SceneInfo()

@@ -76,8 +76,12 @@ def test_seed_helper_range():
 
 def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.cornell_box(64, 48).describe()
+    # four box clusters: the room (5 walls), the two rotated boxes, the light rectangle
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
-                    "lds_bytes": 18 * 112, "n_sphere_nodes": 0, "n_triangle_bvh_nodes": 0}
+                    "lds_bytes": 18 * 112 + 4 * 112, "n_sphere_nodes": 0, "n_triangle_bvh_nodes": 0,
+                    "n_box_clusters": 4, "pair_free_mask": 0}
+    boxes = g.Scene.random_boxes(16, 8, 4, seed=1).describe()
+    assert boxes["n_box_clusters"] == 6 and boxes["pair_free_mask"] == 0  # room, 4 boxes, light
     soup = g.Scene.random_triangles(16, 8, 1000).describe()
     assert soup["n_triangle_bvh_nodes"] == 2 * 1036 - 1 and soup["lds_bytes"] == 0
 
@@ -87,7 +91,9 @@ def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.random_spheres(64, 48, 1000).describe()
     assert info["n_sphere_nodes"] == bvh_nodes(1000)
     assert info["n_triangle_pairs"] == 6
-    # only the triangle pairs are staged; the sphere BVH is read with scalar loads
-    assert info["lds_bytes"] == 6 * 112
+    # only the triangle pairs (+ the room and light box clusters) are staged;
+    # the sphere BVH is read with scalar loads
+    assert info["n_box_clusters"] == 2
+    assert info["lds_bytes"] == 6 * 112 + 2 * 112
     big = g.Scene.random_spheres(16, 8, 5000).describe()
-    assert big["lds_bytes"] == 6 * 112 and big["n_sphere_nodes"] == bvh_nodes(5000)
+    assert big["lds_bytes"] == 6 * 112 + 2 * 112 and big["n_sphere_nodes"] == bvh_nodes(5000)

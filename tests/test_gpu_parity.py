@@ -186,7 +186,7 @@ def test_errors_are_status_codes():
         assert out.shape == (8, 16, 4)
 
 
-@pytest.mark.parametrize("layout", ["single", "smem", "sorted", "pairsmem", "bvh"])
+@pytest.mark.parametrize("layout", ["single", "smem", "sorted", "pairsmem", "bvh", "pairs"])
 def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
     """The single-triangle LDS layout, the global (scalar-load) layout and the
     octant-sorted path kernel give the same bits as the default pair kernel
@@ -235,6 +235,18 @@ def test_random_quads_pair_layout_and_culling_bit_exact(seed):
     with Renderer(s, seeds=sd) as r:
         out = r.render(RenderParams(spp=16, bounces=4))
     assert_parity(out, oracle_lib.render(s, sd, 16, 4), f"quads seed {seed}")
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_random_rotated_boxes_clusters_bit_exact(seed):
+    """Box clusters on 4 randomly rotated boxes in the room:
+    the per-lane slab test + candidate faces must give the brute-force bits."""
+    s = Scene.random_boxes(48, 32, 4, seed=seed)
+    assert s.describe()["n_box_clusters"] == 6
+    sd = seed_splitmix(48, 32, key=100 + seed)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=4, bounces=4))
+    assert_parity(out, oracle_lib.render(s, sd, 4, 4), f"boxes{seed}")
 
 
 def test_render_progressive_async_equals_single_shot():

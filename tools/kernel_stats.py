@@ -26,4 +26,8 @@ for q, n in enumerate(names):
               "tested_frac": tested / max(visits, 1), "lane_util": lanes / max(64 * tested, 1),
               "div_blocks_per_tested": divs / max(tested, 1),
               "tested_per_sample": tested * 64 / samples}
+q, rounds, rl, ql = st[12:16]
+out["clusters"] = {"queries_per_wave": q, "rounds_per_query": rounds / max(q, 1),
+                   "lanes_per_round": rl / max(rounds, 1), "lanes_per_query": ql / max(q, 1),
+                   "candidate_tests_per_sample": rl / samples}
 print(json.dumps(out, indent=1))
