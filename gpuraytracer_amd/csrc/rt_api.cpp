@@ -359,6 +359,9 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
     rt::MisParams K;
     memset(&K, 0, sizeof(K));
     K.tri_isect = c->d_tri_isect;
+    K.clusters = c->d_clusters;
+    K.nC = (uint32_t)(c->scene.clusters.size() / (4 * rt::kCluF4));
+    K.pair_free = c->scene.pair_free_mask;
     K.pair_isect = c->d_pair_isect;
     K.mis_shade = c->d_mis_shade;
     K.u_tab = c->d_mis_tab;

@@ -67,6 +67,8 @@ struct MisParams {
     const uint32_t* tri_perm;
     uint32_t nTN;
     const float4* pair_isect;  // kPairF4 float4 per pair, or null
+    const float4* clusters;    // box clusters (as KParams), or null
+    uint32_t nC, pair_free;
     const float4* mis_shade;   // 3 float4 per triangle (MisShade)
     const float4* u_tab;       // 3 float4 per MIS sample index i < S (Halton table)
     float4* out;               // (sum over camera rays, camera_rays) per pixel, or null

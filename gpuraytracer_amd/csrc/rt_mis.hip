@@ -282,12 +282,18 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         sv.tri = nullptr;
         sv.pair = nullptr;
     } else if (GEO != kGeoTriGlobal) {
-        const uint32_t ng4 = (GEO == kGeoPairLds) ? kPairF4 * sv.nP : 3u * sv.nT;
-        const float4* src = (GEO == kGeoPairLds) ? P.pair_isect : P.tri_isect;
+        constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu;
+        const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
+        const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
+        if (GEO == kGeoPairClu)  // box clusters after the pair records
+            for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
+        sv.clu = lds + ng4;
+        sv.nC = P.nC;
+        sv.pair_free = P.pair_free;
     } else {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
@@ -360,7 +366,10 @@ hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
     if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) {
         hipLaunchKernelGGL(mis_kernel<kGeoTriBvh>, grid, dim3(kBlockThreads), 0, stream, P);
     } else if (lds_ok) {
-        if (pairs)
+        const size_t lds_clu = lds + kCluF4 * P.nC * sizeof(float4);
+        if (pairs && P.nC > 0 && mem == SceneMem::kAuto && lds_clu <= kMaxLdsBytes)
+            hipLaunchKernelGGL(mis_kernel<kGeoPairClu>, grid, dim3(kBlockThreads), lds_clu, stream, P);
+        else if (pairs)
             hipLaunchKernelGGL(mis_kernel<kGeoPairLds>, grid, dim3(kBlockThreads), lds, stream, P);
         else
             hipLaunchKernelGGL(mis_kernel<kGeoTriLds>, grid, dim3(kBlockThreads), lds, stream, P);

@@ -94,7 +94,7 @@ def test_mis_device_outputs_match_host():
     assert_same(only8.cpu().numpy(), host8, "rgba8 only")
 
 
-@pytest.mark.parametrize("layout", ["single", "smem"])
+@pytest.mark.parametrize("layout", ["single", "smem", "pairs"])
 def test_mis_scene_layouts_bit_exact(layout, monkeypatch):
     monkeypatch.setenv("RTPT_SCENE_MEM", layout)
     s = Scene.cornell_box_mis(40, 24)
@@ -103,6 +103,17 @@ def test_mis_scene_layouts_bit_exact(layout, monkeypatch):
     ref, ref8 = oracle_lib.render_mis(s, 2, 12)
     assert_same(out, ref, layout)
     assert_same(out8, ref8, layout)
+
+
+def test_mis_box_clusters_rotated_boxes_bit_exact():
+    """MIS queries through the box clusters on randomly rotated boxes."""
+    s = Scene.random_boxes(40, 24, 4, seed=5)
+    assert s.describe()["n_box_clusters"] == 6
+    with Renderer(s) as r:
+        out, out8 = r.render_mis(MisParams(camera_rays=2, mis_samples=9))
+    ref, ref8 = oracle_lib.render_mis(s, 2, 9)
+    assert_same(out, ref, "boxes")
+    assert_same(out8, ref8, "boxes")
 
 
 def test_mis_errors_are_status_codes():
