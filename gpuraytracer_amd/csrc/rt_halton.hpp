@@ -65,6 +65,9 @@ constexpr uint32_t kMagicS[24] = {20, 21, 22, 23, 23, 25, 25, 25, 25, 26, 26, 27
 constexpr int kSmallIndexBits = 21;
 template <uint32_t D>
 __device__ __forceinline__ float halton_small(uint32_t i) {
+#ifdef RT_TIMING_NO_HALTON  // timing-only experiment (share of the Halton digits), NOT exact
+    return (float)((i * (2654435761u + 2u * D)) >> 8) * (1.0f / 16777216.0f);
+#endif
     constexpr uint32_t b = kPrimes[D];
     if constexpr (b == 2) {
         return (float)(__builtin_bitreverse32(i) >> (32 - kSmallIndexBits)) *

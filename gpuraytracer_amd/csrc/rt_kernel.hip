@@ -295,13 +295,21 @@ size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 #ifndef RT_MIN_WAVES_PER_EU_SPH
 #define RT_MIN_WAVES_PER_EU_SPH 8
 #endif
+#ifndef RT_MIN_WAVES_PER_EU_CLU
+// box-cluster kernel: 7 waves/SIMD runs as fast as 8 and spills 6 VGPRs
+// instead of 30 (HBM traffic 146 MB instead of 19 GB per 1080p launch)
+#define RT_MIN_WAVES_PER_EU_CLU 7
+#endif
 // L lanes per pixel (1, 4 or 16: more lanes when the launch has few pixels,
 // e.g. one GPU's share of a multi-GPU frame): lane `sub` of a pixel's
 // group traces samples n = r*L + sub of round r, and after every round the L
 // colours are shuffled within the wave and added to the pixel's sum in sample
 // order n — the same sequence of fp32 additions as one lane per pixel.
 template <int B, int GEO, bool SPH, bool SMALL, int L = 1>
-__global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH : RT_MIN_WAVES_PER_EU) void path_trace_kernel(KParams P) {
+__global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH
+                                               : (GEO == kGeoPairClu ? RT_MIN_WAVES_PER_EU_CLU
+                                                                     : RT_MIN_WAVES_PER_EU))
+void path_trace_kernel(KParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
     sv.nT = P.nT;
