@@ -609,7 +609,9 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     const bool bvh = info->n_triangles > rt::kTriBvhMinTriangles ||
                      std::min(lds, lds_single) > rt::kMaxLdsBytes;
     info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
-    const size_t lds_clu = lds + rt::kCluF4 * sizeof(float) * 4 * info->n_box_clusters;
+    // box clusters are staged after the pairs in triangle-only scenes
+    const size_t lds_clu =
+        lds + (info->n_spheres ? 0u : rt::kCluF4 * sizeof(float) * 4 * info->n_box_clusters);
     info->lds_bytes = (!bvh && lds <= rt::kMaxLdsBytes)
                           ? (uint32_t)(lds_clu <= rt::kMaxLdsBytes ? lds_clu : lds)
                           : 0u;

@@ -91,9 +91,9 @@ def test_scene_layout_uses_shared_edge_pairs():
     info = g.Scene.random_spheres(64, 48, 1000).describe()
     assert info["n_sphere_nodes"] == bvh_nodes(1000)
     assert info["n_triangle_pairs"] == 6
-    # only the triangle pairs (+ the room and light box clusters) are staged;
+    # only the triangle pairs are staged (box clusters: triangle-only scenes);
     # the sphere BVH is read with scalar loads
     assert info["n_box_clusters"] == 2
-    assert info["lds_bytes"] == 6 * 112 + 2 * 112
+    assert info["lds_bytes"] == 6 * 112
     big = g.Scene.random_spheres(16, 8, 5000).describe()
-    assert big["lds_bytes"] == 6 * 112 + 2 * 112 and big["n_sphere_nodes"] == bvh_nodes(5000)
+    assert big["lds_bytes"] == 6 * 112 and big["n_sphere_nodes"] == bvh_nodes(5000)
