@@ -1,7 +1,7 @@
 // rt_halton.hpp — the Halton radical inverse of the path-tracing kernels
-// (RTrace/sampling.metal:97-122), compile-time dimension forms shared by
-// rt_kernel.hip and rt_stream.hip.  Every form is bit-identical to the
-// reference loop.
+// (RTrace/sampling.metal:97-122), compile-time dimension forms shared by the
+// path-tracing kernels.  Every form is bit-identical to the reference loop
+// (DESIGN.md §3.3).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -90,8 +90,101 @@ __device__ __forceinline__ float halton_small(uint32_t i) {
     }
 }
 
-template <uint32_t D, bool SMALL>
-__device__ __forceinline__ float halton_dim(uint32_t i) {
+// ---- low-digit tables --------------------------------------
+// The reference adds the digits lowest first, so after the k lowest digits its
+// running sum depends only on i mod b^k.  A workgroup fills T_D[v] (v < b^k,
+// the loop's r after k digit steps of v; digits past v's own add +0) in LDS
+// with the same fp32 operations, and halton_tab continues from T_D[i mod b^k]
+// with the remaining digits of i / b^k: the same sum, bit for bit.  k per
+// dimension fits the tables in ~17 KB of LDS (the dims of bounces 0-1 and the
+// light sample of bounce 2; 22 of the 73 digit steps of a 3-bounce sample).
+constexpr int kTabDigits[24] = {0, 7, 4, 3, 2, 2, 0, 2, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+// q = floor(i / b^k) = (i * M) >> S for every i < 2^21 (exhaustively verified
+// by tests/test_oracle.py::test_halton_table_magic, which parses this table)
+constexpr uint32_t kTabM[24] = {0, 1963863, 1717987, 782611, 2218475, 198547, 0, 2974355, 1014879,
+                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+constexpr uint32_t kTabS[24] = {0, 32, 30, 28, 28, 25, 0, 30, 29,
+                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+constexpr uint32_t ipow(uint32_t b, int k) { return k == 0 ? 1u : b * ipow(b, k - 1); }
+constexpr uint32_t tab_size(int D) { return kTabDigits[D] ? ipow(kPrimes[D], kTabDigits[D]) : 0u; }
+constexpr uint32_t tab_offset(int D) { return D == 0 ? 0u : tab_offset(D - 1) + tab_size(D - 1); }
+constexpr uint32_t kHaltonTabFloats = tab_offset(24);
+// f = invB^k as the reference's loop forms it (f = f * invB, k times)
+constexpr float f_after(uint32_t b, int k) {
+    float f = 1.0f;
+    for (int j = 0; j < k; ++j) f = f * (1.0f / (float)b);
+    return f;
+}
+
+template <uint32_t D>
+__device__ __forceinline__ void fill_halton_table(float* tab, uint32_t tid, uint32_t nthreads) {
+    constexpr uint32_t b = kPrimes[D];
+    constexpr int k = kTabDigits[D];
+    constexpr float invB = 1.0f / (float)b;
+    constexpr uint32_t off = tab_offset(D), size = tab_size(D);  // compile time
+    for (uint32_t v0 = tid; v0 < size; v0 += nthreads) {
+        uint32_t v = v0;
+        float f = 1.0f;
+        float r = 0.0f;
+#pragma unroll
+        for (int j = 0; j < k; ++j) {
+            f = f * invB;
+            r = r + f * (float)(v % b);
+            v = v / b;
+        }
+        tab[off + v0] = r;
+    }
+}
+
+// All tables; every thread of the workgroup calls it (then a barrier).
+__device__ __forceinline__ void fill_halton_tables(float* tab, uint32_t tid, uint32_t nthreads) {
+    fill_halton_table<1>(tab, tid, nthreads);
+    fill_halton_table<2>(tab, tid, nthreads);
+    fill_halton_table<3>(tab, tid, nthreads);
+    fill_halton_table<4>(tab, tid, nthreads);
+    fill_halton_table<5>(tab, tid, nthreads);
+    fill_halton_table<7>(tab, tid, nthreads);
+    fill_halton_table<8>(tab, tid, nthreads);
+    static_assert(kHaltonTabFloats == 2187 + 625 + 343 + 121 + 169 + 361 + 529, "table list");
+}
+
+// halton_small<D> for i < 2^21 starting from the low-digit table.
+template <uint32_t D>
+__device__ __forceinline__ float halton_tab(uint32_t i, const float* tab) {
+    constexpr uint32_t b = kPrimes[D];
+    constexpr int k = kTabDigits[D];
+    constexpr int nd = halton_digits(b, kSmallIndexBits);
+    constexpr float invB = 1.0f / (float)b;
+    constexpr uint32_t bk = ipow(b, k), TM = kTabM[D], TS = kTabS[D], off = tab_offset(D);
+    static_assert(k > 0 && k < nd, "dimension without a table");
+    uint32_t q;
+    if constexpr (TS >= 32)
+        q = rt_mulhi_u24(i, TM) >> (TS - 32);
+    else
+        q = __builtin_amdgcn_alignbit(rt_mulhi_u24(i, TM), rt_mul_u24(i, TM), TS);
+    const uint32_t low = (uint32_t)((int32_t)i + rt_mul_i24((int32_t)q, -(int32_t)bk));
+    float r = tab[off + low];
+    constexpr float fk = f_after(b, k);  // compile time (a run-time call needs a stack)
+    float f = fk;
+    constexpr uint32_t M = kMagicM[D], S = kMagicS[D];
+    i = q;
+#pragma unroll
+    for (int j = k; j < nd; ++j) {
+        f = f * invB;
+        const uint32_t q2 = __builtin_amdgcn_alignbit(rt_mulhi_u24(i, M), rt_mul_u24(i, M), S);
+        const uint32_t digit = (uint32_t)((int32_t)i + rt_mul_i24((int32_t)q2, -(int32_t)b));
+        r = r + f * (float)digit;
+        i = q2;
+    }
+    return r;
+}
+
+// TAB: the kernel staged the low-digit tables (SMALL indices only).
+template <uint32_t D, bool SMALL, bool TAB = false>
+__device__ __forceinline__ float halton_dim(uint32_t i, const float* tab = nullptr) {
+#ifndef RT_TIMING_NO_HALTON
+    if constexpr (TAB && SMALL && kTabDigits[D] > 0) return halton_tab<D>(i, tab);
+#endif
     if (SMALL) return halton_small<D>(i);
     return halton<D>(i);
 }

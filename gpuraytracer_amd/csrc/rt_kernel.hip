@@ -69,8 +69,8 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     const f3 p = (s.o + s.d * t) + N * 1e-3f;              // :67
 
     // sampleAreaLight (sampling.metal:198-236), dims 2+5b, 3+5b (:72-74)
-    const float ux = halton_dim<2 + 5 * b, SMALL>(s.i) * 2.0f - 1.0f;
-    const float uy = halton_dim<3 + 5 * b, SMALL>(s.i) * 2.0f - 1.0f;
+    const float ux = halton_dim<2 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab) * 2.0f - 1.0f;
+    const float uy = halton_dim<3 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab) * 2.0f - 1.0f;
     const f3 lcen = ld_f3(P.light_center);
     const f3 q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
     f3 L = q - p;
@@ -84,8 +84,8 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     const f3 seg_lo{fminf(p.x, q.x), fminf(p.y, q.y), fminf(p.z, q.z)};
     const f3 seg_hi{fmaxf(p.x, q.x), fmaxf(p.y, q.y), fmaxf(p.z, q.z)};
     if (FUSE && b + 1 < B) {
-        const float cu = halton_dim<4 + 5 * b, SMALL>(s.i);           // :93-94
-        const float cv = halton_dim<5 + 5 * b, SMALL>(s.i);
+        const float cu = halton_dim<4 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);           // :93-94
+        const float cv = halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
         float sp, cp;
         sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
         const float ct = sqrtf(cv);
@@ -102,8 +102,8 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     if (!any_hit<GEO, SPH, (b == 0 && RT_SPH_PACKET) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + lc * s.thr;                        // :87-89
     if (b + 1 < B) {                                       // last direction never traced
-        const float cu = halton_dim<4 + 5 * b, SMALL>(s.i);           // :93-94
-        const float cv = halton_dim<5 + 5 * b, SMALL>(s.i);
+        const float cu = halton_dim<4 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);           // :93-94
+        const float cv = halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
         float sp, cp;
         sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
         const float ct = sqrtf(cv);
@@ -324,8 +324,13 @@ void path_trace_kernel(KParams P) {
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
-        if (GEO == kGeoPairClu)  // box clusters after the pair records
+        if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
+            sv.htab = reinterpret_cast<const float*>(lds + ng4 + kCluF4 * P.nC);
+            if (SMALL)
+                fill_halton_tables(reinterpret_cast<float*>(lds + ng4 + kCluF4 * P.nC), threadIdx.x,
+                                   kBlockThreads);
+        }
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
@@ -382,7 +387,8 @@ void path_trace_kernel(KParams P) {
         s.acc = f3{0.0f, 0.0f, 0.0f};
         {
             s.i = seed + (P.sample_base + n);
-            const float jx = halton_dim<0, SMALL>(s.i), jy = halton_dim<1, SMALL>(s.i);   // :39-40
+            const float jx = halton_dim<0, SMALL>(s.i);                                // :39-40
+            const float jy = halton_dim<1, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
             // generateCameraRay (sampling.metal:125-157)
             const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
             const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
@@ -632,9 +638,9 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
     // pressure measured 4.6 % slower than the culled pair loop (config 4)
     size_t lds_total = lds_bytes;
     if (geo == kGeoPairLds && P.nC > 0 && P.nS == 0 && mem == SceneMem::kAuto &&
-        lds_bytes + kCluF4 * P.nC * sizeof(float4) <= kMaxLdsBytes) {
+        lds_bytes + kCluF4 * P.nC * sizeof(float4) + kHaltonTabFloats * sizeof(float) <= kMaxLdsBytes) {
         geo = kGeoPairClu;
-        lds_total = lds_bytes + kCluF4 * P.nC * sizeof(float4);
+        lds_total = lds_bytes + kCluF4 * P.nC * sizeof(float4) + kHaltonTabFloats * sizeof(float);
     }
     // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the
     // Cornell 1080p workload (barrier + occupancy cost).

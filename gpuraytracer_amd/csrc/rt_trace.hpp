@@ -156,6 +156,7 @@ struct SceneView {
     const float4* clu;        // box clusters, 4 float4 each (kGeoPairClu)
     uint32_t nC;
     uint32_t pair_free;       // pairs in no cluster: tested by every lane
+    const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
 };
 
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the

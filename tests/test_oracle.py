@@ -275,6 +275,52 @@ def test_halton_small_magic_table():
         assert np.array_equal((i * np.uint64(m)) >> np.uint64(s), i // np.uint64(b)), b
 
 
+def test_halton_table_magic():
+    """The low-digit table split of rt_halton.hpp (kTabDigits/kTabM/kTabS):
+    q = i / b^k by a 24-bit magic multiply, exact for every index < 2^21."""
+    import re
+    src = open(os.path.join(os.path.dirname(GOLDEN), "..", "gpuraytracer_amd", "csrc",
+                            "rt_halton.hpp")).read()
+    grab = lambda name: [int(v) for v in re.search(name + r"\[24\] = \{([^}]*)\}", src)
+                         .group(1).split(",")]
+    K, M, S = grab("kTabDigits"), grab("kTabM"), grab("kTabS")
+    primes = [2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73,
+              79, 83, 89]
+    i = np.arange(1 << 21, dtype=np.uint64)
+    for d in range(24):
+        if K[d] == 0:
+            continue
+        bk = primes[d] ** K[d]
+        assert M[d] < (1 << 24) and bk < (1 << 23)
+        assert np.array_equal((i * np.uint64(M[d])) >> np.uint64(S[d]), i // np.uint64(bk)), d
+
+
+def test_halton_low_digit_split_is_the_reference_sum():
+    """T[i mod b^k] continued with the digits of i / b^k is the reference loop
+    (sampling.metal:107-122) bit for bit (numpy float32, same operation order)."""
+    f32 = np.float32
+    for b, k in ((3, 7), (5, 4), (7, 3), (11, 2)):
+        inv = f32(1) / f32(b)
+        idx = np.random.default_rng(b).integers(0, 1 << 21, 4000, dtype=np.int64)
+        for i0 in idx:
+            ref_f, ref_r, i = f32(1), f32(0), int(i0)
+            while i > 0:
+                ref_f = f32(ref_f * inv)
+                ref_r = f32(ref_r + f32(ref_f * f32(i % b)))
+                i //= b
+            v, f, r = int(i0) % b ** k, f32(1), f32(0)
+            for _ in range(k):
+                f = f32(f * inv)
+                r = f32(r + f32(f * f32(v % b)))
+                v //= b
+            i = int(i0) // b ** k
+            while i > 0:
+                f = f32(f * inv)
+                r = f32(r + f32(f * f32(i % b)))
+                i //= b
+            assert r.tobytes() == ref_r.tobytes(), (b, i0)
+
+
 # ---- MIS integrator (Sources/gpuRaytracer/shaders.metal) ----------------------------
 def test_mis_scene_builder_equals_oracle_and_main_swift():
     s = Scene.cornell_box_mis(800, 600)
