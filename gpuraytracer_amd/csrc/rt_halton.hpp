@@ -96,15 +96,15 @@ __device__ __forceinline__ float halton_small(uint32_t i) {
 // the loop's r after k digit steps of v; digits past v's own add +0) in LDS
 // with the same fp32 operations, and halton_tab continues from T_D[i mod b^k]
 // with the remaining digits of i / b^k: the same sum, bit for bit.  k per
-// dimension fits the tables in ~17 KB of LDS (the dims of bounces 0-1 and the
-// light sample of bounce 2; 22 of the 73 digit steps of a 3-bounce sample).
-constexpr int kTabDigits[24] = {0, 7, 4, 3, 2, 2, 0, 2, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+// dimension fits the tables in ~18 KB of LDS (the camera jitter and bounces
+// 0-1; 24 of the 73 digit steps of a 3-bounce sample).
+constexpr int kTabDigits[24] = {0, 6, 4, 3, 2, 2, 0, 2, 2, 2, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 // q = floor(i / b^k) = (i * M) >> S for every i < 2^21 (exhaustively verified
 // by tests/test_oracle.py::test_halton_table_magic, which parses this table)
-constexpr uint32_t kTabM[24] = {0, 1963863, 1717987, 782611, 2218475, 198547, 0, 2974355, 1014879,
-                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-constexpr uint32_t kTabS[24] = {0, 32, 30, 28, 28, 25, 0, 30, 29,
-                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+constexpr uint32_t kTabM[24] = {0, 1472897, 1717987, 782611, 2218475, 198547, 0, 2974355, 1014879,
+                                2553489, 2234635, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+constexpr uint32_t kTabS[24] = {0, 30, 30, 28, 28, 25, 0, 30, 29,
+                                31, 31, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 constexpr uint32_t ipow(uint32_t b, int k) { return k == 0 ? 1u : b * ipow(b, k - 1); }
 constexpr uint32_t tab_size(int D) { return kTabDigits[D] ? ipow(kPrimes[D], kTabDigits[D]) : 0u; }
 constexpr uint32_t tab_offset(int D) { return D == 0 ? 0u : tab_offset(D - 1) + tab_size(D - 1); }
@@ -145,7 +145,10 @@ __device__ __forceinline__ void fill_halton_tables(float* tab, uint32_t tid, uin
     fill_halton_table<5>(tab, tid, nthreads);
     fill_halton_table<7>(tab, tid, nthreads);
     fill_halton_table<8>(tab, tid, nthreads);
-    static_assert(kHaltonTabFloats == 2187 + 625 + 343 + 121 + 169 + 361 + 529, "table list");
+    fill_halton_table<9>(tab, tid, nthreads);
+    fill_halton_table<10>(tab, tid, nthreads);
+    static_assert(kHaltonTabFloats == 729 + 625 + 343 + 121 + 169 + 361 + 529 + 841 + 961,
+                  "table list");
 }
 
 // halton_small<D> for i < 2^21 starting from the low-digit table.
