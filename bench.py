@@ -210,7 +210,9 @@ def main():
         traffic = None
         prof = load_profile_json("pmc_summary.json")
         compute = None
-        if prof and prof.get("workload") == workload and prof.get("n_gpus", 1) == 1 and world == 1:
+        from gpuraytracer_amd.srchash import kernel_source_sha
+        if (prof and prof.get("workload") == workload and prof.get("n_gpus", 1) == 1 and world == 1
+                and prof.get("kernel_src_sha") == kernel_source_sha()):
             traffic = prof.get("hbm_bytes_per_launch")
             if prof.get("sq_insts_valu_per_launch"):
                 wi = prof["sq_insts_valu_per_launch"] / (kernel_ms * 1e-3)

@@ -191,3 +191,4 @@ def _load():
 
 
 lib = _load()
+

@@ -182,11 +182,14 @@ __device__ __forceinline__ float halton_tab(uint32_t i, const float* tab) {
     return r;
 }
 
-// TAB: the kernel staged the low-digit tables (SMALL indices only).
+// TAB: the kernel may stage the low-digit tables (SMALL indices only); tab is
+// null (wave-uniform) when this launch has too few samples per lane to pay for
+// filling them.
 template <uint32_t D, bool SMALL, bool TAB = false>
 __device__ __forceinline__ float halton_dim(uint32_t i, const float* tab = nullptr) {
 #ifndef RT_TIMING_NO_HALTON
-    if constexpr (TAB && SMALL && kTabDigits[D] > 0) return halton_tab<D>(i, tab);
+    if constexpr (TAB && SMALL && kTabDigits[D] > 0)
+        if (tab != nullptr) return halton_tab<D>(i, tab);
 #endif
     if (SMALL) return halton_small<D>(i);
     return halton<D>(i);

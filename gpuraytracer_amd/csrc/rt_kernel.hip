@@ -295,6 +295,7 @@ size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 #ifndef RT_MIN_WAVES_PER_EU_SPH
 #define RT_MIN_WAVES_PER_EU_SPH 8
 #endif
+constexpr uint32_t kHaltonTabMinRounds = 8;  // samples per lane below which no tables
 #ifndef RT_MIN_WAVES_PER_EU_CLU
 // box-cluster kernel: 7 waves/SIMD runs as fast as 8 and spills 6 VGPRs
 // instead of 30 (HBM traffic 146 MB instead of 19 GB per 1080p launch)
@@ -326,8 +327,11 @@ void path_trace_kernel(KParams P) {
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
-            sv.htab = reinterpret_cast<const float*>(lds + ng4 + kCluF4 * P.nC);
-            if (SMALL)
+            // tables only when every lane traces enough samples to amortise the
+            // fill (~700 VALU per thread): config 1 (1 spp) runs without them
+            const bool tab = SMALL && (P.spp + L - 1) / L >= kHaltonTabMinRounds;
+            sv.htab = tab ? reinterpret_cast<const float*>(lds + ng4 + kCluF4 * P.nC) : nullptr;
+            if (tab)
                 fill_halton_tables(reinterpret_cast<float*>(lds + ng4 + kCluF4 * P.nC), threadIdx.x,
                                    kBlockThreads);
         }

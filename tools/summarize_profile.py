@@ -49,7 +49,10 @@ def rows(pattern):
 
 def main():
     d = sys.argv[1]
-    out = {"workload": bench_workload(sys.argv[2:]), "n_gpus": 1, "kernel": None}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from gpuraytracer_amd.srchash import kernel_source_sha
+    out = {"workload": bench_workload(sys.argv[2:]), "n_gpus": 1, "kernel": None,
+           "kernel_src_sha": kernel_source_sha()}
     durs = []
     for r in rows(os.path.join(d, "trace", "**", "*kernel_trace.csv")):
         if KERNEL in r.get("Kernel_Name", ""):
