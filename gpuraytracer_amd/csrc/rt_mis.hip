@@ -261,7 +261,7 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
 }  // namespace
 
 #ifndef RT_MIS_WAVES_PER_EU
-#define RT_MIS_WAVES_PER_EU 7  // occupancy over spills: 3 waves 37.5 ms, 7 waves 27.6 ms, 8 waves 28.5 ms
+#define RT_MIS_WAVES_PER_EU 5  // box clusters: 4/5/6/7 waves 24.8/24.5/24.4/25.8 ms (pair loop: 3 waves 37.5, 7 waves 27.6, 8 waves 28.5)
 #endif
 template <int GEO>
 __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel(MisParams P) {
