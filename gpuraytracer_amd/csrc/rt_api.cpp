@@ -29,6 +29,8 @@ struct rt_ctx {
     float4* d_tri_shade = nullptr;
     float4* d_pair_isect = nullptr;
     float4* d_clusters = nullptr;
+    uint32_t* d_sph_lds = nullptr;
+    uint16_t* d_sph_lds_id = nullptr;
     float4* d_sph_isect = nullptr;
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
@@ -105,6 +107,8 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_tri_shade);
     (void)hipFree(c->d_pair_isect);
     (void)hipFree(c->d_clusters);
+    (void)hipFree(c->d_sph_lds);
+    (void)hipFree(c->d_sph_lds_id);
     (void)hipFree(c->d_sph_isect);
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_sph_nodes);
@@ -200,6 +204,8 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.nC = (uint32_t)(c->scene.clusters.size() / (4 * rt::kCluF4));
     K.pair_free = c->scene.pair_free_mask;
     K.sph_isect = c->d_sph_isect;
+    K.sph_lds = c->scene.sph_lds.empty() ? nullptr : c->d_sph_lds;
+    K.sph_lds_id = c->d_sph_lds_id;
     K.sph_shade = c->d_sph_shade;
     K.sph_nodes = c->d_sph_nodes;
     K.sph_perm = c->d_sph_perm;
@@ -485,6 +491,8 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
             (e = upload(&c->d_tri_shade, s.tri_shade.data(), s.tri_shade.size() * sizeof(rt::TriShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_pair_isect, s.pair_isect.data(), s.pair_isect.size() * sizeof(rt::PairIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_clusters, s.clusters.data(), s.clusters.size() * sizeof(float), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_lds, s.sph_lds.data(), s.sph_lds.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_lds_id, s.sph_lds_id.data(), s.sph_lds_id.size() * sizeof(uint16_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_nodes, s.sph_nodes.data(), s.sph_nodes.size() * sizeof(rt::BvhNode), c->stream)) != hipSuccess ||
@@ -609,6 +617,13 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     const bool bvh = info->n_triangles > rt::kTriBvhMinTriangles ||
                      std::min(lds, lds_single) > rt::kMaxLdsBytes;
     info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
+    {
+        const size_t sb = s.sph_lds.size() * 4 + ((s.sph_lds_id.size() * 2 + 3) & ~(size_t)3);
+        info->sphere_bvh_lds_bytes =
+            (!s.sph_lds.empty() && lds <= rt::kMaxLdsBytes && lds + sb <= rt::kSphLdsMaxBytes)
+                ? (uint32_t)(lds + sb)
+                : 0u;
+    }
     // box clusters are staged after the pairs in triangle-only scenes
     const size_t lds_clu =
         lds + (info->n_spheres ? 0u : rt::kCluF4 * sizeof(float) * 4 * info->n_box_clusters);

@@ -306,11 +306,18 @@ constexpr uint32_t kHaltonTabMinRounds = 8;  // samples per lane below which no 
 // group traces samples n = r*L + sub of round r, and after every round the L
 // colours are shuffled within the wave and added to the pixel's sum in sample
 // order n — the same sequence of fp32 additions as one lane per pixel.
+// Workgroup size: 1024 threads (4x4 waves) when the sphere BVH is staged in
+// LDS, so one ~72 KB copy serves 16 waves; 256 (2x2 waves) otherwise.
+constexpr uint32_t block_threads(int geo) { return geo == kGeoSphLds ? 1024u : kBlockThreads; }
+constexpr uint32_t waves_per_row(int geo) { return geo == kGeoSphLds ? 4u : 2u; }
+
 template <int B, int GEO, bool SPH, bool SMALL, int L = 1>
-__global__ __launch_bounds__(kBlockThreads, SPH ? RT_MIN_WAVES_PER_EU_SPH
-                                               : (GEO == kGeoPairClu ? RT_MIN_WAVES_PER_EU_CLU
-                                                                     : RT_MIN_WAVES_PER_EU))
+__global__ __launch_bounds__(block_threads(GEO),
+                             SPH ? RT_MIN_WAVES_PER_EU_SPH
+                                 : (GEO == kGeoPairClu ? RT_MIN_WAVES_PER_EU_CLU
+                                                       : RT_MIN_WAVES_PER_EU))
 void path_trace_kernel(KParams P) {
+    constexpr uint32_t NT = block_threads(GEO), WR = waves_per_row(GEO);
     extern __shared__ float4 lds[];
     SceneView sv;
     sv.nT = P.nT;
@@ -321,19 +328,30 @@ void path_trace_kernel(KParams P) {
         sv.pair = P.pair_isect;
     } else if (GEO != kGeoTriGlobal) {
         // Stage the intersection records once per workgroup.
-        constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu;
+        constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu || GEO == kGeoSphLds;
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
-        for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
+        if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) + entry ids after the pairs
+            const uint32_t ne = 2u * P.nN;
+            const uint4* es = reinterpret_cast<const uint4*>(P.sph_lds);
+            uint4* ed = reinterpret_cast<uint4*>(lds + ng4);
+            for (uint32_t k = threadIdx.x; k < ne; k += NT) ed[k] = es[k];
+            const uint32_t* is = reinterpret_cast<const uint32_t*>(P.sph_lds_id);
+            uint32_t* id = reinterpret_cast<uint32_t*>(lds + ng4 + ne);
+            for (uint32_t k = threadIdx.x; k < (ne + 1) / 2; k += NT) id[k] = is[k];
+            sv.sent = ed;
+            sv.sid = reinterpret_cast<const uint16_t*>(id);
+        }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
-            for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
+            for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
             // tables only when every lane traces enough samples to amortise the
             // fill (~700 VALU per thread): config 1 (1 spp) runs without them
             const bool tab = SMALL && (P.spp + L - 1) / L >= kHaltonTabMinRounds;
             sv.htab = tab ? reinterpret_cast<const float*>(lds + ng4 + kCluF4 * P.nC) : nullptr;
             if (tab)
                 fill_halton_tables(reinterpret_cast<float*>(lds + ng4 + kCluF4 * P.nC), threadIdx.x,
-                                   kBlockThreads);
+                                   NT);
         }
         __syncthreads();
         sv.tri = lds;
@@ -359,8 +377,8 @@ void path_trace_kernel(KParams P) {
     const uint32_t kWX = (L == 1) ? 8u : P.wave_w, kWY = (64u / L) / kWX;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t pix = lane / L, sub = lane % L;
-    const uint32_t x = blockIdx.x * (2 * kWX) + (wave & 1u) * kWX + (pix % kWX);
-    const uint32_t j = blockIdx.y * (2 * kWY) + (wave >> 1) * kWY + (pix / kWX);
+    const uint32_t x = blockIdx.x * (WR * kWX) + (wave % WR) * kWX + (pix % kWX);
+    const uint32_t j = blockIdx.y * (WR * kWY) + (wave / WR) * kWY + (pix / kWX);
     if (x >= (uint32_t)P.W || j >= P.row_count) return;  // a pixel's L lanes leave together
     const uint32_t y = P.row_start + j * P.row_step;
     const size_t o = (size_t)j * (size_t)P.W + x;
@@ -373,7 +391,7 @@ void path_trace_kernel(KParams P) {
     }
     // L > 1: the pixel's running sum lives in LDS (its group leader adds to it),
     // which keeps three VGPRs free across the path traversal
-    __shared__ float lum_s[L > 1 ? 3 * (kBlockThreads / L) : 1];
+    __shared__ float lum_s[L > 1 ? 3 * (NT / L) : 1];
     const uint32_t slot = threadIdx.x / L;
     if (L > 1 && sub == 0) {
         lum_s[3 * slot] = lum.x;
@@ -545,6 +563,12 @@ inline int lanes_per_pixel(const KParams& P) {
     return P.spp >= 4 ? 4 : 1;
 }
 
+// Dynamic LDS above 64 KB must be allowed per kernel (the compact sphere BVH).
+inline hipError_t allow_lds(const void* kernel, size_t bytes) {
+    if (bytes <= 65536) return hipSuccess;
+    return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 template <int B, int GEO, bool SPH, bool SMALL, int L>
 hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     KParams Q = P;
@@ -552,9 +576,14 @@ hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     // when the rows are interleaved (row_step > 1), which keeps a wave's camera
     // rays adjacent in the image (N = 8 share: 10,822 -> 11,211 Msamples/s)
     Q.wave_w = (P.row_step > 1) ? 64u / L : (L == 4 ? 4u : 2u);
-    const uint32_t TX = 2 * Q.wave_w, TY = 2 * ((64u / L) / Q.wave_w);
+    constexpr uint32_t WR = waves_per_row(GEO);
+    const uint32_t TX = WR * Q.wave_w, TY = WR * ((64u / L) / Q.wave_w);
     const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);
-    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL, L>), grid, dim3(kBlockThreads),
+    if (GEO == kGeoSphLds) {
+        const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL, L>, lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL, L>), grid, dim3(block_threads(GEO)),
                        (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,
                        stream, Q);
     return hipGetLastError();
@@ -567,8 +596,13 @@ hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
         if (lpp == 16) return launch_tl<B, GEO, SPH, SMALL, 16>(P, lds_bytes, stream);
         if (lpp == 4) return launch_tl<B, GEO, SPH, SMALL, 4>(P, lds_bytes, stream);
     }
-    const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
-    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(kBlockThreads),
+    constexpr uint32_t T = 8u * waves_per_row(GEO);  // 8x8-pixel waves
+    const dim3 grid((P.W + T - 1) / T, (P.row_count + T - 1) / T);
+    if (GEO == kGeoSphLds) {
+        const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL>, lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(block_threads(GEO)),
                        (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,
                        stream, P);
     return hipGetLastError();
@@ -580,6 +614,9 @@ hipError_t launch_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     if constexpr (GEO == kGeoPairClu)  // triangle-only scenes (launch_path_trace)
         return small ? launch_t<B, GEO, false, true>(P, lds_bytes, stream)
                      : launch_t<B, GEO, false, false>(P, lds_bytes, stream);
+    if constexpr (GEO == kGeoSphLds)  // sphere scenes only
+        return small ? launch_t<B, GEO, true, true>(P, lds_bytes, stream)
+                     : launch_t<B, GEO, true, false>(P, lds_bytes, stream);
     if (P.nS > 0)
         return small ? launch_t<B, GEO, true, true>(P, lds_bytes, stream)
                      : launch_t<B, GEO, true, false>(P, lds_bytes, stream);
@@ -611,6 +648,7 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
     switch (geo) {
         case kGeoPairLds: return launch_g<B, kGeoPairLds>(P, lds_bytes, stream);
         case kGeoPairClu: return launch_g<B, kGeoPairClu>(P, lds_bytes, stream);
+        case kGeoSphLds: return launch_g<B, kGeoSphLds>(P, lds_bytes, stream);
         case kGeoPairSmem: return launch_g<B, kGeoPairSmem>(P, lds_bytes, stream);
         case kGeoTriBvh: return launch_g<B, kGeoTriBvh>(P, lds_bytes, stream);
         case kGeoTriLds: return launch_g<B, kGeoTriLds>(P, lds_bytes, stream);
@@ -637,10 +675,18 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
     // triangle BVH whenever rt_create built one (kTriBvhMinTriangles or no LDS fit),
     // unless another layout is forced
     if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) geo = kGeoTriBvh;
+    size_t lds_total = lds_bytes;
+    // sphere BVH in LDS (1024-thread workgroups, two per CU) when it fits
+    if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto) {
+        const size_t b = lds_bytes + 2u * P.nN * 16u + ((2u * P.nN * 2u + 3u) & ~3u);
+        if (b <= kSphLdsMaxBytes) {
+            geo = kGeoSphLds;
+            lds_total = b;
+        }
+    }
     // box clusters whenever rt_create found some; not with
     // spheres, where the sphere walks dominate and the cluster code's register
     // pressure measured 4.6 % slower than the culled pair loop (config 4)
-    size_t lds_total = lds_bytes;
     if (geo == kGeoPairLds && P.nC > 0 && P.nS == 0 && mem == SceneMem::kAuto &&
         lds_bytes + kCluF4 * P.nC * sizeof(float4) + kHaltonTabFloats * sizeof(float) <= kMaxLdsBytes) {
         geo = kGeoPairClu;

@@ -14,6 +14,9 @@ constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
 constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
+// dynamic LDS of the sphere-BVH-in-LDS kernel: two 1024-thread workgroups per
+// CU share 160 KB with their static per-pixel sums (3 KB at 4 lanes per pixel)
+constexpr size_t kSphLdsMaxBytes = 76 * 1024;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
@@ -28,6 +31,8 @@ struct KParams {
     const float4* sph_nodes;  // 2 float4 per sphere-BVH node (BvhNode)
     const uint32_t* sph_perm; // BVH leaf order -> sphere id
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
+    const uint32_t* sph_lds;  // compact sphere BVH (2 layouts x nN x 16 B) for LDS, or null
+    const uint16_t* sph_lds_id;  // sphere id per compact entry
     const float4* tri_nodes;  // triangle BVH (rt_lbvh.hip): 8 layouts x nTN nodes, or null
     const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
     const uint32_t* tri_perm; // BVH leaf order -> triangle id

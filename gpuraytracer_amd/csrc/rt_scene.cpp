@@ -350,6 +350,56 @@ struct BvhBuild {
     }
 };
 
+// fp16 bits of x rounded toward -inf (dir < 0) or +inf (dir > 0)
+static uint16_t half_dir(float x, int dir) {
+    const _Float16 h = (_Float16)x;  // round to nearest even
+    uint16_t b;
+    memcpy(&b, &h, 2);
+    const float back = (float)h;
+    const bool neg = (b & 0x8000u) != 0, zero = (b & 0x7FFFu) == 0;
+    if (dir < 0 && back > x) b = zero ? 0x8001u : (neg ? b + 1 : b - 1);
+    if (dir > 0 && back < x) b = zero ? 0x0001u : (neg ? b - 1 : b + 1);
+    return b;
+}
+
+static void build_sphere_lds(CompiledScene* out) {
+    out->sph_lds.clear();
+    out->sph_lds_id.clear();
+    const uint32_t nn = out->sph_layout_nodes;
+    if (nn == 0 || nn > 0x7FFFu || out->sph_isect.size() > 0xFFFFu) return;
+    std::vector<uint32_t> ent;
+    std::vector<uint16_t> ids;
+    for (int oct : {0, 7}) {
+        const BvhNode* L = out->sph_nodes.data() + (size_t)oct * nn;
+        for (uint32_t k = 0; k < nn; ++k) {
+            const BvhNode& n = L[k];
+            uint32_t w[4];
+            if (n.leaf == 0) {
+                uint16_t h[6];
+                for (int a = 0; a < 3; ++a) {
+                    if (!isfinite(n.lo[a]) || !isfinite(n.hi[a])) return;
+                    h[a] = half_dir(n.lo[a], -1);
+                    h[3 + a] = half_dir(n.hi[a], +1);
+                }
+                w[0] = h[0] | (uint32_t)h[1] << 16;
+                w[1] = h[2] | (uint32_t)h[3] << 16;
+                w[2] = h[4] | (uint32_t)h[5] << 16;
+                w[3] = n.escape | 0x80000000u;
+                ids.push_back(0);
+            } else {
+                if ((n.leaf >> 24) != 1u || n.escape != k + 1) return;  // one sphere per leaf
+                const uint32_t first = n.leaf & 0xFFFFFFu;
+                memcpy(w, out->sph_isect[first].q, 16);
+                if (w[3] & 0x80000000u) return;  // r*r is never negative
+                ids.push_back((uint16_t)out->sph_perm[first]);
+            }
+            ent.insert(ent.end(), w, w + 4);
+        }
+    }
+    out->sph_lds.swap(ent);
+    out->sph_lds_id.swap(ids);
+}
+
 static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint32_t n,
                              float margin) {
     out->sph_isect.clear();
@@ -383,6 +433,7 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
         const float q[4] = {sp.center.x, sp.center.y, sp.center.z, r2};
         memcpy(out->sph_isect[k].q, q, sizeof(q));
     }
+    build_sphere_lds(out);
 }
 
 // Pair layout: triangles (2k, 2k+1) with the same v0 and one common edge

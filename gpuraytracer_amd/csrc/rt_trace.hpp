@@ -138,9 +138,10 @@ enum Geo : int {
     kGeoTriBvh = 5,     // GPU-built triangle BVH (rt_lbvh.hip), records from global
     kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
     kGeoPairClu = 6,    // pair records in LDS + box clusters
+    kGeoSphLds = 7,     // pair records + the compact sphere BVH in LDS (1024-thread workgroups)
 };
 
-constexpr bool geo_pairs(int g) { return g == kGeoPairLds || g == kGeoPairSmem; }
+constexpr bool geo_pairs(int g) { return g == kGeoPairLds || g == kGeoPairSmem || g == kGeoSphLds; }
 
 struct SceneView {
     const float4* tri;        // 3 float4 per triangle (single layout)
@@ -157,6 +158,8 @@ struct SceneView {
     uint32_t nC;
     uint32_t pair_free;       // pairs in no cluster: tested by every lane
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
+    const uint4* sent;        // compact sphere BVH entries in LDS (kGeoSphLds), 2 layouts
+    const uint16_t* sid;      // sphere id of each entry (leaves)
 };
 
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
@@ -290,6 +293,87 @@ __device__ __forceinline__ bool sphere_any(const float4* __restrict__ node,
             }
             idx = next;
         }
+    }
+    return found;
+}
+
+// Sphere-BVH walks over the compact LDS entries (rt_scene.cpp build_sphere_lds):
+// the same stackless depth-first walk and (t, id) ranking as sphere_closest /
+// sphere_any, with fp16 boxes rounded outward (still conservative) and the
+// sphere of a leaf stored in the entry itself (a leaf's escape is the next
+// entry).  Two layouts: near child first for (+,+,+) and for (-,-,-); a ray
+// takes the one matching most of its direction signs.
+__device__ __forceinline__ float h2f(uint32_t b16) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)b16);
+}
+
+__device__ __forceinline__ uint32_t lds_layout(f3 d) {
+    return __builtin_popcount(octant(d)) >= 2 ? 1u : 0u;
+}
+
+__device__ __forceinline__ bool lds_node_hit(const uint4& e, const RayBox& rb, float tmin,
+                                             float tmax) {
+    const float4 n0 = make_float4(h2f(e.x & 0xFFFFu), h2f(e.x >> 16), h2f(e.y & 0xFFFFu), 0.0f);
+    const float4 n1 = make_float4(h2f(e.y >> 16), h2f(e.z & 0xFFFFu), h2f(e.z >> 16), 0.0f);
+    return node_hit(n0, n1, rb, tmin, tmax);
+}
+
+template <bool PACKET>
+__device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint16_t* ids,
+                                                   uint32_t nN, uint32_t nT, f3 o, f3 d,
+                                                   float tmin, float& best, int& id) {
+    const float a = dot(d, d);
+    const RayBox rb = ray_box(o, d);
+    const uint32_t lay = PACKET ? wave_uniform(lds_layout(d)) : lds_layout(d);
+    ent += lay * nN;
+    ids += lay * nN;
+    uint32_t idx = 0;
+    while (idx < nN) {
+        const uint4 e = ent[idx];
+        uint32_t next = idx + 1;
+        if (e.w & 0x80000000u) {  // inner node (wave-uniform for PACKET)
+            const bool h = lds_node_hit(e, rb, tmin, best);
+            if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) next = e.w & 0x7FFFFFFFu;
+        } else {  // leaf: the sphere (c, r*r)
+            float t;
+            if (sph_test(make_float4(__uint_as_float(e.x), __uint_as_float(e.y),
+                                     __uint_as_float(e.z), __uint_as_float(e.w)),
+                         o, d, a, tmin, 3.0e38f, &t) && t <= best) {
+                const int s = (int)(nT + ids[idx]);
+                if (t < best || s < id) {
+                    best = t;
+                    id = s;
+                }
+            }
+        }
+        idx = PACKET ? wave_uniform(next) : next;
+    }
+}
+
+template <bool PACKET>
+__device__ __forceinline__ bool sphere_any_lds(const uint4* ent, uint32_t nN, f3 o, f3 d,
+                                               float tmin, float tmax) {
+    const float a = dot(d, d);
+    const RayBox rb = ray_box(o, d);
+    const uint32_t lay = PACKET ? wave_uniform(lds_layout(d)) : lds_layout(d);
+    ent += lay * nN;
+    bool found = false;
+    uint32_t idx = 0;
+    while (idx < nN) {
+        const uint4 e = ent[idx];
+        uint32_t next = idx + 1;
+        if (e.w & 0x80000000u) {
+            const bool h = !found && lds_node_hit(e, rb, tmin, tmax);
+            if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) next = e.w & 0x7FFFFFFFu;
+        } else {
+            float t;
+            found = found || sph_test(make_float4(__uint_as_float(e.x), __uint_as_float(e.y),
+                                                  __uint_as_float(e.z), __uint_as_float(e.w)),
+                                      o, d, a, tmin, tmax, &t);
+            if (!PACKET && found) return true;
+            if (PACKET && __builtin_amdgcn_ballot_w64(!found) == 0) break;
+        }
+        idx = PACKET ? wave_uniform(next) : next;
     }
     return found;
 }
@@ -566,7 +650,10 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
             }
         }
     }
-    if (SPH) sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
+    if (SPH && GEO == kGeoSphLds)
+        sphere_closest_lds<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
+    else if (SPH)
+        sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
     *t_io = best;
     return id;
 }
@@ -619,6 +706,7 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
                 return true;
         }
     }
+    if (SPH && GEO == kGeoSphLds) return sphere_any_lds<PACKET>(sv.sent, sv.nN, o, d, tmin, tmax);
     if (SPH) return sphere_any<PACKET>(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
     return false;
 }

@@ -79,7 +79,7 @@ def test_scene_layout_uses_shared_edge_pairs():
     # four box clusters: the room (5 walls), the two rotated boxes, the light rectangle
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
                     "lds_bytes": 18 * 112 + 4 * 112, "n_sphere_nodes": 0, "n_triangle_bvh_nodes": 0,
-                    "n_box_clusters": 4, "pair_free_mask": 0}
+                    "n_box_clusters": 4, "pair_free_mask": 0, "sphere_bvh_lds_bytes": 0}
     boxes = g.Scene.random_boxes(16, 8, 4, seed=1).describe()
     assert boxes["n_box_clusters"] == 6 and boxes["pair_free_mask"] == 0  # room, 4 boxes, light
     soup = g.Scene.random_triangles(16, 8, 1000).describe()
@@ -95,5 +95,7 @@ def test_scene_layout_uses_shared_edge_pairs():
     # the sphere BVH is read with scalar loads
     assert info["n_box_clusters"] == 2
     assert info["lds_bytes"] == 6 * 112
+    # the compact sphere BVH (2 layouts x 1999 entries x 16 B + 2-B ids) goes to LDS
+    assert info["sphere_bvh_lds_bytes"] == 6 * 112 + 2 * 1999 * 16 + 2 * 1999 * 2
     big = g.Scene.random_spheres(16, 8, 5000).describe()
-    assert big["lds_bytes"] == 6 * 112 and big["n_sphere_nodes"] == bvh_nodes(5000)
+    assert big["lds_bytes"] == 6 * 112 and big["sphere_bvh_lds_bytes"] == 0 and big["n_sphere_nodes"] == bvh_nodes(5000)

@@ -106,6 +106,35 @@ def test_duplicate_spheres_tie_to_lower_id():
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), "duplicates")
 
 
+@pytest.mark.parametrize("layout", ["auto", "pairs"])
+def test_sphere_bvh_lds_and_global_walks_bit_exact(layout, monkeypatch):
+    """auto: the compact fp16 sphere BVH in LDS (1024-thread workgroups);
+    pairs: the 8-layout BVH read from global memory.  Both are the oracle."""
+    if layout != "auto":
+        monkeypatch.setenv("RTPT_SCENE_MEM", layout)
+    s = Scene.random_spheres(40, 24, 700, seed=13)
+    sd = seed_splitmix(40, 24, key=13)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=3, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, 3, 3), f"spheres700-{layout}")
+
+
+def test_sphere_bvh_lds_fp16_boxes_far_spheres():
+    """Spheres out to |x| ~ 7000 (fp16 box corners 4 units apart, rounded
+    outward): the LDS walk must still return the brute-force hits."""
+    s = Scene.random_spheres(40, 24, 200, seed=17)
+    for k in range(0, 200, 2):  # every other sphere far away and large
+        sp = s.spheres[k]
+        sp.center.x, sp.center.y, sp.center.z = (sp.center.x * 2900.0, sp.center.y * 2900.0,
+                                                 -abs(sp.center.z) * 2900.0 - 50.0)
+        sp.radius = sp.radius * 2900.0
+    assert s.describe()["sphere_bvh_lds_bytes"] > 0
+    sd = seed_splitmix(40, 24, key=17)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=2, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, 2, 3), "far spheres")
+
+
 def test_large_sphere_scene_bvh():
     # 5000 spheres: deep BVH (2047 nodes), ties and leaves far beyond the 1000-sphere case
     s = Scene.random_spheres(24, 16, 5000, seed=9)
