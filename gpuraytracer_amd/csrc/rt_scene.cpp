@@ -645,6 +645,11 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
             const double c[3] = {best.u[a].x, best.u[a].y, best.u[a].z};
             if (c[a] == 1.0) flags |= 1u << a;
         }
+        // container (bit 3): world-aligned with room inside (the kernel skips
+        // it for shadow segments that stay inside, rt_trace.hpp)
+        bool roomy = flags == 7u;
+        for (int a = 0; a < 3; ++a) roomy = roomy && best.hi[a] - best.lo[a] > 1e-3 * fmax(1.0, ext);
+        if (roomy) flags |= 8u;
         // padding per axis: tol_n, plus the margin if some face lies across it
         double pad[3];
         for (int a = 0; a < 3; ++a) {

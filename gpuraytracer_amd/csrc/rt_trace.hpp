@@ -473,6 +473,12 @@ __device__ __forceinline__ bool tri_bvh_any(const float4* __restrict__ node,
 // its plane's interval [t_plane -/+ w] meets [Tlo, Thi] — in a box that is the
 // face the ray enters through and the one it leaves through (two or three more
 // near an edge or corner).  Only speed depends on the rounding here.
+// SEG (shadow any-hit): a container cluster (flags bit 3: all axes world axes,
+// a box with volume, e.g. the room) is skipped for the whole wave when every
+// lane's segment [o, o + d*tmax] lies inside the box shrunk to more than the
+// normal tolerance from each face plane: the box is convex, so the segment
+// stays away from every face and no face can accept a hit.
+template <bool SEG = false>
 __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o, f3 d, float tmin,
                                                        float tmax) {
     constexpr float kEps = 1.52587890625e-05f;  // 2^-16 relative slack
@@ -480,12 +486,28 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
     const RayBox rb = ray_box(o, d);
     const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
     const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
+    f3 e{0.0f, 0.0f, 0.0f};
+    if (SEG) e = o + d * tmax;
     uint32_t mask = 0;
     for (uint32_t c = 0; c < sv.nC; ++c) {
         const float4* r = sv.clu + kCluF4 * c;
         const float4 H = r[3], M0 = r[4], M1 = r[5], W = r[6];
         const uint32_t flags = __float_as_uint(H.w);
         const float hi[3] = {H.x, H.y, H.z}, wf[3] = {W.x, W.y, W.z};
+        if (SEG && (flags & 8u)) {  // wave-uniform
+            const float lo[3] = {r[0].w, r[1].w, r[2].w};
+            const float oo[3] = {o.x, o.y, o.z}, ee[3] = {e.x, e.y, e.z};
+            bool inside = true;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                // lo' + w = face plane + tol_n; 2^-16 relative slack for the
+                // rounding of o + d*tmax and of the bounds
+                const float in_lo = lo[a] + wf[a] + kEps * (fabsf(lo[a]) + fabsf(ee[a]));
+                const float in_hi = hi[a] - wf[a] - kEps * (fabsf(hi[a]) + fabsf(ee[a]));
+                inside = inside && oo[a] > in_lo && oo[a] < in_hi && ee[a] > in_lo && ee[a] < in_hi;
+            }
+            if (__builtin_amdgcn_ballot_w64(!inside) == 0) continue;
+        }
         float en[3], ex[3], ida[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -567,7 +589,7 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
         const uint32_t k = (uint32_t)__builtin_ctz(free);
         pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);
     }
-    uint32_t cand = cluster_candidates(sv, o, d, tmin, *best);
+    uint32_t cand = cluster_candidates<ANY>(sv, o, d, tmin, *best);
     RT_STAT(12, 1);
     RT_STAT(15, __popcll(__ballot(1)));
     while (cand != 0u && !(ANY && *id >= 0)) {
