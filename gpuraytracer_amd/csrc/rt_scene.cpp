@@ -275,8 +275,23 @@ struct BvhBuild {
     const SphereGPU* sph;
     float margin;
     uint32_t leaf_max = 1;  // measured best for config 4 (RTPT_BVH_LEAF sweep 1..8)
+    bool sah = true;        // SAH splits (RTPT_BVH_SAH=0: median of the longest axis)
     std::vector<uint32_t> ids;
     std::vector<Node> tree;
+
+    void grow(uint32_t id, float lo[3], float hi[3]) const {
+        const SphereGPU& s = sph[id];
+        const float c[3] = {s.center.x, s.center.y, s.center.z};
+        const float r = fabsf(s.radius);
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], c[a] - r);
+            hi[a] = fmaxf(hi[a], c[a] + r);
+        }
+    }
+    static double area(const float lo[3], const float hi[3]) {
+        const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+        return x * y + y * z + z * x;
+    }
 
     void bounds(uint32_t b, uint32_t e, float lo[3], float hi[3], bool centroids) const {
         for (int a = 0; a < 3; ++a) {
@@ -313,13 +328,47 @@ struct BvhBuild {
         int axis = 0;
         for (int a = 1; a < 3; ++a)
             if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
-        const uint32_t mid = b + (e - b) / 2;
-        std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e,
-                         [&](uint32_t x, uint32_t y) {
-                             const float cx[3] = {sph[x].center.x, sph[x].center.y, sph[x].center.z};
-                             const float cy[3] = {sph[y].center.x, sph[y].center.y, sph[y].center.z};
-                             return cx[axis] < cy[axis] || (cx[axis] == cy[axis] && x < y);
-                         });
+        uint32_t mid = b + (e - b) / 2;
+        auto by_axis = [&](int ax) {
+            return [this, ax](uint32_t x, uint32_t y) {
+                const float cx[3] = {sph[x].center.x, sph[x].center.y, sph[x].center.z};
+                const float cy[3] = {sph[y].center.x, sph[y].center.y, sph[y].center.z};
+                return cx[ax] < cy[ax] || (cx[ax] == cy[ax] && x < y);
+            };
+        };
+        if (sah) {
+            // exact SAH sweep over the centroid order of every axis:
+            // cost(split) = area(left) * n_left + area(right) * n_right
+            double best_cost = INFINITY;
+            int best_axis = axis;
+            uint32_t best_mid = mid;
+            const uint32_t n = e - b;
+            std::vector<double> right_area(n);
+            for (int a = 0; a < 3; ++a) {
+                std::sort(ids.begin() + b, ids.begin() + e, by_axis(a));
+                float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (uint32_t k = e; k-- > b + 1;) {  // right part = [k, e)
+                    grow(ids[k], lo, hi);
+                    right_area[k - b] = area(lo, hi);
+                }
+                for (int q = 0; q < 3; ++q) {
+                    lo[q] = INFINITY;
+                    hi[q] = -INFINITY;
+                }
+                for (uint32_t k = b + 1; k < e; ++k) {  // left part = [b, k)
+                    grow(ids[k - 1], lo, hi);
+                    const double c = area(lo, hi) * (k - b) + right_area[k - b] * (e - k);
+                    if (c < best_cost) {
+                        best_cost = c;
+                        best_axis = a;
+                        best_mid = k;
+                    }
+                }
+            }
+            axis = best_axis;
+            mid = best_mid;
+        }
+        std::nth_element(ids.begin() + b, ids.begin() + mid, ids.begin() + e, by_axis(axis));
         const uint32_t l = build(b, mid);
         const uint32_t r = build(mid, e);
         tree[me].axis = axis;
@@ -410,6 +459,7 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
     BvhBuild bb;
     bb.sph = spheres;
     bb.margin = margin;
+    if (const char* sm = getenv("RTPT_BVH_SAH")) bb.sah = atoi(sm) != 0;  // tuning knob
     if (const char* lm = getenv("RTPT_BVH_LEAF")) {  // tuning knob (speed only)
         const int v = atoi(lm);
         if (v >= 1 && v <= 255) bb.leaf_max = (uint32_t)v;
