@@ -482,20 +482,18 @@ template <bool SEG = false>
 __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o, f3 d, float tmin,
                                                        float tmax) {
     constexpr float kEps = 1.52587890625e-05f;  // 2^-16 relative slack
-    // per-ray terms of world-aligned box axes: t = lo * invd - o * invd
-    const RayBox rb = ray_box(o, d);
-    const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
-    const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
-    f3 e{0.0f, 0.0f, 0.0f};
-    if (SEG) e = o + d * tmax;
-    uint32_t mask = 0;
-    for (uint32_t c = 0; c < sv.nC; ++c) {
-        const float4* r = sv.clu + kCluF4 * c;
-        const float4 H = r[3], M0 = r[4], M1 = r[5], W = r[6];
-        const uint32_t flags = __float_as_uint(H.w);
-        const float hi[3] = {H.x, H.y, H.z}, wf[3] = {W.x, W.y, W.z};
-        if (SEG && (flags & 8u)) {  // wave-uniform
-            const float lo[3] = {r[0].w, r[1].w, r[2].w};
+    // containers the whole wave's segments stay inside (wave-uniform bit mask),
+    // decided before the slab terms are live
+    uint32_t skip = 0;
+    if (SEG) {
+        const f3 e = o + d * tmax;
+        for (uint32_t c = 0; c < sv.nC; ++c) {
+            const float4* r = sv.clu + kCluF4 * c;
+            const float4 H = r[3];
+            if (!(__float_as_uint(H.w) & 8u)) continue;
+            const float4 W = r[6];
+            const float lo[3] = {r[0].w, r[1].w, r[2].w}, hi[3] = {H.x, H.y, H.z};
+            const float wf[3] = {W.x, W.y, W.z};
             const float oo[3] = {o.x, o.y, o.z}, ee[3] = {e.x, e.y, e.z};
             bool inside = true;
 #pragma unroll
@@ -506,8 +504,20 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
                 const float in_hi = hi[a] - wf[a] - kEps * (fabsf(hi[a]) + fabsf(ee[a]));
                 inside = inside && oo[a] > in_lo && oo[a] < in_hi && ee[a] > in_lo && ee[a] < in_hi;
             }
-            if (__builtin_amdgcn_ballot_w64(!inside) == 0) continue;
+            if (__builtin_amdgcn_ballot_w64(!inside) == 0) skip |= 1u << c;
         }
+    }
+    // per-ray terms of world-aligned box axes: t = lo * invd - o * invd
+    const RayBox rb = ray_box(o, d);
+    const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
+    const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
+    uint32_t mask = 0;
+    for (uint32_t c = 0; c < sv.nC; ++c) {
+        if (SEG && ((skip >> c) & 1u)) continue;
+        const float4* r = sv.clu + kCluF4 * c;
+        const float4 H = r[3], M0 = r[4], M1 = r[5], W = r[6];
+        const uint32_t flags = __float_as_uint(H.w);
+        const float hi[3] = {H.x, H.y, H.z}, wf[3] = {W.x, W.y, W.z};
         float en[3], ex[3], ida[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
