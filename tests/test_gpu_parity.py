@@ -200,6 +200,28 @@ def test_full_size_1080p_properties():
     assert_parity(one[539:541], band, "1080p rows 539-540")
 
 
+def test_full_frame_1080p_bit_exact_vs_oracle():
+    """The headline workload's frame (config 2 geometry, 1920x1080, 3 bounces)
+    at 8 spp, every pixel against the C oracle (~17 M samples on 16 host
+    threads): box clusters, Halton tables and 4 lanes per pixel at full size."""
+    s = Scene.cornell_box(1920, 1080)
+    sd = seed_splitmix(1920, 1080)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=8, bounces=3))
+    ref = oracle_lib.render(s, sd, 8, 3, threads=16)
+    assert_parity(out, ref, "1080p x 8 spp full frame")
+
+
+def test_spheres_frame_bit_exact_vs_oracle():
+    """Config-4 scene (1000 spheres, LDS SAH BVH) on a 240x135 frame x 8 spp."""
+    s = Scene.random_spheres(240, 135, 1000, seed=42)
+    sd = seed_splitmix(240, 135)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=8, bounces=3))
+    ref = oracle_lib.render(s, sd, 8, 3, threads=16)
+    assert_parity(out, ref, "spheres 240x135 x 8 spp")
+
+
 def test_errors_are_status_codes():
     s = Scene.cornell_box(16, 8)
     with Renderer(s) as r:
