@@ -250,9 +250,11 @@ def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
     assert_parity(out, oracle_lib.render(s, sd, 3, 3), layout)
 
 
-def random_quad_scene(w, h, n_quads, seed):
+def random_quad_scene(w, h, n_quads, seed, twist=0.0):
     """Cornell camera/light + random planar-ish quads as shared-edge pairs:
-    stresses the pair layout and the conservative segment culling."""
+    stresses the pair layout and the conservative segment culling.  twist > 0
+    lifts the 4th corner of every other quad off its plane (such a quad is in
+    no box cluster: every lane tests it)."""
     base = Scene.cornell_box(w, h)
     rng = np.random.default_rng(seed)
     n = 2 * n_quads + 2
@@ -264,6 +266,8 @@ def random_quad_scene(w, h, n_quads, seed):
         a *= rng.uniform(0.05, 1.5) / np.linalg.norm(a)
         b *= rng.uniform(0.05, 1.5) / np.linalg.norm(b)
         P = [c, c + a, c + a + b, c + b]
+        if twist and q % 2:
+            P[3] = P[3] + twist * np.cross(a, b) / np.linalg.norm(np.cross(a, b))
         for t, tri in enumerate([(P[0], P[1], P[2]), (P[0], P[2], P[3])]):
             k = 2 * q + t
             for v in range(3):
@@ -298,6 +302,19 @@ def test_random_rotated_boxes_clusters_bit_exact(seed):
     with Renderer(s, seeds=sd) as r:
         out = r.render(RenderParams(spp=4, bounces=4))
     assert_parity(out, oracle_lib.render(s, sd, 4, 4), f"boxes{seed}")
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_twisted_quads_free_pairs_and_clusters_bit_exact(seed):
+    """Non-planar quads fall out of the box clusters (tested by every lane),
+    planar ones form flat clusters: both kinds in one query."""
+    s = random_quad_scene(48, 32, 20, seed, twist=0.2)
+    info = s.describe()
+    assert info["pair_free_mask"] != 0 and info["n_box_clusters"] > 0
+    sd = seed_splitmix(48, 32, key=seed)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=4, bounces=4))
+    assert_parity(out, oracle_lib.render(s, sd, 4, 4), f"twisted{seed}")
 
 
 def test_render_progressive_async_equals_single_shot():
