@@ -700,6 +700,15 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
         bool roomy = flags == 7u;
         for (int a = 0; a < 3; ++a) roomy = roomy && best.hi[a] - best.lo[a] > 1e-3 * fmax(1.0, ext);
         if (roomy) flags |= 8u;
+        // single face (bit 4): the kernel takes it whenever the padded box is hit
+        int nfaces = 0;
+        uint32_t all_faces = 0;
+        for (int sl = 0; sl < 6; ++sl)
+            if (best.slot_pair[sl] >= 0) {
+                ++nfaces;
+                all_faces |= 1u << best.slot_pair[sl];
+            }
+        if (nfaces == 1) flags |= 16u;
         // padding per axis: tol_n, plus the margin if some face lies across it
         double pad[3];
         for (int a = 0; a < 3; ++a) {
@@ -724,7 +733,7 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
         cl.push_back(bits(flags));
         for (int sl = 0; sl < 6; ++sl)  // pair bit of each face slot (2*axis + side)
             cl.push_back(bits(best.slot_pair[sl] < 0 ? 0u : 1u << best.slot_pair[sl]));
-        cl.push_back(0.0f);
+        cl.push_back(bits(all_faces));
         cl.push_back(0.0f);
         // face-plane half width factor per axis: the face plane lies pad inside
         // the padded slab, an accepted hit within tol_n of it
@@ -732,7 +741,18 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
         cl.push_back(0.0f);
         k0 = k1;
     }
-    out->clusters.swap(cl);
+    // single-face clusters last: the kernel's main cluster loop stops at the
+    // first one and a lean loop slab-tests the rest (rt_trace.hpp)
+    std::vector<float> multi, single;
+    const size_t rec = 28;  // floats per cluster record (rt_kernel.hpp kCluF4 = 7 float4)
+    for (size_t c = 0; c < cl.size() / rec; ++c) {
+        uint32_t flags;
+        memcpy(&flags, &cl[c * rec + 15], 4);
+        std::vector<float>& dst = (flags & 16u) ? single : multi;
+        dst.insert(dst.end(), cl.begin() + c * rec, cl.begin() + (c + 1) * rec);
+    }
+    multi.insert(multi.end(), single.begin(), single.end());
+    out->clusters.swap(multi);
     out->pair_free_mask = free_mask;
 }
 

@@ -105,10 +105,11 @@ struct CompiledScene {
     std::vector<uint16_t> sph_lds_id;   // 2 layouts x sph_layout_nodes
     // Box clusters over the pair records: 28 floats each,
     // (u0.xyz, lo0) (u1.xyz, lo1) (u2.xyz, lo2) (hi0, hi1, hi2, flags)
-    // (m0, m1, m2, m3) (m4, m5, 0, 0) (w0, w1, w2, 0): an oriented box (padded
+    // (m0, m1, m2, m3) (m4, m5, all, 0) (w0, w1, w2, 0): an oriented box (padded
     // extents) whose faces hold consecutive pair records; m_s = bit of the pair
-    // on face slot s = 2*axis + side (0: none); flags bit a = axis a is world
-    // axis a (+); w_a = face-plane half width factor of axis a.
+    // on face slot s = 2*axis + side (0: none), all = their union; flags bit a
+    // = axis a is world axis a (+), bit 3 = container, bit 4 = single face;
+    // w_a = face-plane half width factor of axis a.
     std::vector<float> clusters;
     uint32_t pair_free_mask = 0;        // pairs in no cluster (tested by every lane)
     float tri_lo[3], tri_hi[3];         // bounds of the triangle vertices (BVH build)

@@ -512,11 +512,13 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
     const float iv[3] = {rb.invd.x, rb.invd.y, rb.invd.z};
     const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
     uint32_t mask = 0;
-    for (uint32_t c = 0; c < sv.nC; ++c) {
+    uint32_t c = 0;
+    for (; c < sv.nC; ++c) {
         if (SEG && ((skip >> c) & 1u)) continue;
         const float4* r = sv.clu + kCluF4 * c;
         const float4 H = r[3], M0 = r[4], M1 = r[5], W = r[6];
         const uint32_t flags = __float_as_uint(H.w);
+        if (flags & 16u) break;  // single-face clusters come last (rt_scene.cpp)
         const float hi[3] = {H.x, H.y, H.z}, wf[3] = {W.x, W.y, W.z};
         float en[3], ex[3], ida[3];
 #pragma unroll
@@ -554,6 +556,33 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
             cm |= (ex[a] - fmaf(fabsf(ex[a]), kEps, wa) <= thi) ? m_ex : 0u;
         }
         mask |= (tlo <= thi) ? cm : 0u;
+    }
+    // single-face clusters (the light, lone rectangles): the face is a
+    // candidate whenever the padded box is hit (a superset of its face test)
+    for (; c < sv.nC; ++c) {
+        const float4* r = sv.clu + kCluF4 * c;
+        const float4 A0 = r[0], A1 = r[1], A2 = r[2], H = r[3];
+        const uint32_t flags = __float_as_uint(H.w);
+        const float4 A[3] = {A0, A1, A2};
+        const float hi[3] = {H.x, H.y, H.z};
+        float tlo0 = tmin, thi0 = tmax;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float t0, t1;
+            if (flags & (1u << a)) {  // wave-uniform
+                t0 = fmaf(A[a].w, iv[a], -oi[a]);
+                t1 = fmaf(hi[a], iv[a], -oi[a]);
+            } else {
+                const float oa = dot(f3{A[a].x, A[a].y, A[a].z}, o);
+                const float ida = safe_rcp(dot(f3{A[a].x, A[a].y, A[a].z}, d));
+                t0 = (A[a].w - oa) * ida;
+                t1 = (hi[a] - oa) * ida;
+            }
+            tlo0 = fmaxf(tlo0, fminf(t0, t1));
+            thi0 = fminf(thi0, fmaxf(t0, t1));
+        }
+        const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
+        mask |= (tlo <= thi) ? __float_as_uint(r[5].z) : 0u;
     }
     return mask;
 }
