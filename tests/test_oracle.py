@@ -259,40 +259,29 @@ def test_tonemap_matches_image_swift():
     assert list(a[0]) == [0, 212, 255, 255]  # 1.0 -> (2/3)^(1/2.2)*255 = 212
 
 
-def test_halton_small_magic_table():
-    """The kernel's 24-bit magic division (rt_halton.hpp kMagicM/kMagicS) is
-    exact for every index < 2^21, for all 24 Halton bases."""
+def test_halton_float_digits():
+    """rt_halton.hpp digit_step: with c = the smallest float >= 1/n (recip_up),
+    q = floor(fl(x * c)) and digit = fma(q, -n, x) in fp32 are x / n and x mod n
+    for every integer x < 2^21, for all 24 Halton bases and the low-digit table
+    moduli b^k (kTabDigits, parsed from the header)."""
     import re
     src = open(os.path.join(os.path.dirname(GOLDEN), "..", "gpuraytracer_amd", "csrc",
                             "rt_halton.hpp")).read()
-    M = [int(v) for v in re.search(r"kMagicM\[24\] = \{([^}]*)\}", src).group(1).split(",")]
-    S = [int(v) for v in re.search(r"kMagicS\[24\] = \{([^}]*)\}", src).group(1).split(",")]
+    K = [int(v) for v in re.search(r"kTabDigits\[24\] = \{([^}]*)\}", src).group(1).split(",")]
     primes = [2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73,
               79, 83, 89]
-    i = np.arange(1 << 21, dtype=np.uint64)
-    for b, m, s in zip(primes, M, S):
-        assert m < (1 << 24) and s < 32
-        assert np.array_equal((i * np.uint64(m)) >> np.uint64(s), i // np.uint64(b)), b
-
-
-def test_halton_table_magic():
-    """The low-digit table split of rt_halton.hpp (kTabDigits/kTabM/kTabS):
-    q = i / b^k by a 24-bit magic multiply, exact for every index < 2^21."""
-    import re
-    src = open(os.path.join(os.path.dirname(GOLDEN), "..", "gpuraytracer_amd", "csrc",
-                            "rt_halton.hpp")).read()
-    grab = lambda name: [int(v) for v in re.search(name + r"\[24\] = \{([^}]*)\}", src)
-                         .group(1).split(",")]
-    K, M, S = grab("kTabDigits"), grab("kTabM"), grab("kTabS")
-    primes = [2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73,
-              79, 83, 89]
-    i = np.arange(1 << 21, dtype=np.uint64)
-    for d in range(24):
-        if K[d] == 0:
-            continue
-        bk = primes[d] ** K[d]
-        assert M[d] < (1 << 24) and bk < (1 << 23)
-        assert np.array_equal((i * np.uint64(M[d])) >> np.uint64(S[d]), i // np.uint64(bk)), d
+    i = np.arange(1 << 21, dtype=np.int64)
+    x = i.astype(np.float32)
+    for d, b in enumerate(primes):
+        for n in [b] + ([b ** K[d]] if K[d] else []):
+            assert n < (1 << 23)
+            c = np.float32(1) / np.float32(n)
+            if float(c) * n < 1.0:  # exact in double: 24-bit x 23-bit
+                c = np.nextafter(c, np.float32(2))
+            q = np.floor(x * c)  # float32 product, rounded once
+            digit = (x.astype(np.float64) - q.astype(np.float64) * n).astype(np.float32)  # fma: exact
+            assert np.array_equal(q.astype(np.int64), i // n), (b, n)
+            assert np.array_equal(digit.astype(np.int64), i % n), (b, n)
 
 
 def test_halton_low_digit_split_is_the_reference_sum():
