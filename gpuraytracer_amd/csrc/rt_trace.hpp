@@ -541,6 +541,9 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
         const float tlo0 = fmaxf(fmaxf(en[0], en[1]), fmaxf(en[2], tmin));
         const float thi0 = fminf(fminf(ex[0], ex[1]), fminf(ex[2], tmax));
         const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
+#ifndef RT_NO_CLU_WAVE_SKIP
+        if (!__builtin_amdgcn_ballot_w64(tlo <= thi)) continue;  // no lane meets the box
+#endif
         const uint32_t m[6] = {__float_as_uint(M0.x), __float_as_uint(M0.y), __float_as_uint(M0.z),
                                __float_as_uint(M0.w), __float_as_uint(M1.x), __float_as_uint(M1.y)};
         uint32_t cm = 0;
