@@ -28,11 +28,11 @@ __device__ __forceinline__ float halton(uint32_t i) {
     return r;
 }
 
-// Digits of i < 2^bits in base b (compile time).
-constexpr int halton_digits(uint32_t b, int bits) {
+// Digits of every i < imax in base b (compile time).
+constexpr int halton_digits(uint32_t b, uint64_t imax) {
     uint64_t cap = 1;
     int n = 0;
-    while (cap < (1ull << bits)) {
+    while (cap < imax) {
         cap *= b;
         ++n;
     }
@@ -63,15 +63,19 @@ __device__ __forceinline__ float digit_step(float x, float& digit) {
     return q;
 }
 
-// The same radical inverse for i < 2^21 (every reference seed is < 2^20,
-// renderer.swift:100): the loop runs a fixed digit count, fully unrolled, so
+// The same radical inverse for i < kSmallIndexMax = 3^13 (every reference
+// seed is < 2^20, renderer.swift:100, so up to 545k samples per pixel; 3^13
+// rather than 2^21 drops the top digit of bases 3, 5 and 11, which a
+// 2^21 bound would need): the loop runs a fixed digit count, fully unrolled, so
 // f = invB^k folds to compile-time constants and no loop control remains.  The
 // extra iterations past i's last digit add f*0 = +0 to r >= 0: bit-identical.
 // Digits come from float reciprocal multiplies (exact, see recip_up).  Base 2
 // is exact in fp32 at every step (sums of distinct powers of two spanning
 // <= 21 bits), so it equals the bit-reversed index: 3 instructions instead of
 // 21 digit steps.
-constexpr int kSmallIndexBits = 21;
+constexpr uint32_t kSmallIndexMax = 1594323;  // 3^13
+constexpr int kSmallIndexBits = 21;           // base-2 bit-reversal width
+static_assert(kSmallIndexMax <= (1u << kSmallIndexBits), "float digit steps need x < 2^21");
 template <uint32_t D>
 __device__ __forceinline__ float halton_small(uint32_t i) {
 #ifdef RT_TIMING_NO_HALTON  // timing-only experiment (share of the Halton digits), NOT exact
@@ -82,7 +86,7 @@ __device__ __forceinline__ float halton_small(uint32_t i) {
         return (float)(__builtin_bitreverse32(i) >> (32 - kSmallIndexBits)) *
                (1.0f / (float)(1u << kSmallIndexBits));
     } else {
-        constexpr int nd = halton_digits(b, kSmallIndexBits);
+        constexpr int nd = halton_digits(b, kSmallIndexMax);
         constexpr float invB = 1.0f / (float)b;
         float x = (float)i;  // exact
         float f = 1.0f;
@@ -154,12 +158,12 @@ __device__ __forceinline__ void fill_halton_tables(float* tab, uint32_t tid, uin
                   "table list");
 }
 
-// halton_small<D> for i < 2^21 starting from the low-digit table.
+// halton_small<D> for i < kSmallIndexMax starting from the low-digit table.
 template <uint32_t D>
 __device__ __forceinline__ float halton_tab(uint32_t i, const float* tab) {
     constexpr uint32_t b = kPrimes[D];
     constexpr int k = kTabDigits[D];
-    constexpr int nd = halton_digits(b, kSmallIndexBits);
+    constexpr int nd = halton_digits(b, kSmallIndexMax);
     constexpr float invB = 1.0f / (float)b;
     constexpr uint32_t bk = ipow(b, k), off = tab_offset(D);
     static_assert(k > 0 && k < nd, "dimension without a table");

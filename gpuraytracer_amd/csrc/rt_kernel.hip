@@ -610,7 +610,7 @@ hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
 
 template <int B, int GEO>
 hipError_t launch_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
-    const bool small = P.max_index < (1u << kSmallIndexBits);
+    const bool small = P.max_index < kSmallIndexMax;
     if constexpr (GEO == kGeoPairClu)  // triangle-only scenes (launch_path_trace)
         return small ? launch_t<B, GEO, false, true>(P, lds_bytes, stream)
                      : launch_t<B, GEO, false, false>(P, lds_bytes, stream);
@@ -637,7 +637,7 @@ constexpr int kGeoPairSorted = 3;  // pair records + per-bounce octant sort of t
 template <int B>
 hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t stream) {
     if (geo == kGeoPairSorted) {
-        const bool small = P.max_index < (1u << kSmallIndexBits);
+        const bool small = P.max_index < kSmallIndexMax;
         const size_t bytes = lds_bytes + sorted_lds_extra_bytes();
         if (P.nS > 0)
             return small ? launch_sorted_t<B, true, true>(P, bytes, stream)

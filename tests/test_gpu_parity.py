@@ -62,6 +62,23 @@ def test_cornell_vs_oracle_all_bounce_counts(bounces):
     assert_parity(out, oracle_lib.render(s, sd, 5, bounces), f"bounces={bounces}")
 
 
+@pytest.mark.parametrize("top", [3 ** 13 - 1, 3 ** 13])
+def test_halton_index_bound_edges(top):
+    """Largest Halton index 3^13 - 1 (the fixed-digit kernels, kSmallIndexMax in
+    rt_halton.hpp: 13 base-3 digits) and 3^13 (the generic loop), with indices
+    spread over the base-3/5/11 top digits; both bit-exact vs the oracle."""
+    spp = 8
+    W, H = 40, 24
+    rng = np.random.default_rng(top)
+    sd = rng.integers(top - spp + 1 - 400000, top - spp + 2, (H, W), dtype=np.int64)
+    sd[3, 7] = top - spp + 1  # max index = top
+    sd = sd.astype(np.uint32)
+    s = Scene.cornell_box(W, H)
+    with Renderer(s, seeds=sd) as r:
+        out = r.render(RenderParams(spp=spp, bounces=3))
+    assert_parity(out, oracle_lib.render(s, sd, spp, 3), f"top={top}")
+
+
 def test_reference_default_800x600_rows_vs_oracle():
     """The reference's own configuration (800x600, 400 spp, 3 bounces,
     raytrace.metal:24-25 / scene.swift:18) — checked on a band of rows."""
