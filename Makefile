@@ -18,6 +18,10 @@ OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_api.o $(BL
 HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp $(SRC)/rt_halton.hpp
 
 LIB ?= $(PKG)/librtpt.so
+# Hash of every source the library is built from (gpuraytracer_amd/srchash.py),
+# compiled into rt_api.o as rt_build_sha(): the loader refuses a stale binary.
+ALLSRC := $(wildcard $(SRC)/*.hip $(SRC)/*.hpp $(SRC)/*.h $(SRC)/*.cpp include/*.h)
+SRC_SHA := $(shell python3 $(PKG)/srchash.py)
 
 all: $(LIB) $(PKG)/rtrace oracle
 
@@ -29,11 +33,14 @@ $(BLD):
 $(BLD)/%.o: $(SRC)/%.hip $(HDRS) $(SRC)/rt_trace.hpp | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(BLD)/rt_api.o: $(SRC)/rt_api.cpp $(ALLSRC) | $(BLD)
+	$(HOSTCXX) $(HOSTFLAGS) -DRT_SRC_SHA='"$(SRC_SHA)"' -c $< -o $@
+
 $(BLD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BLD)
 	$(HOSTCXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -Wl,--no-undefined
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,--no-undefined
 
 $(PKG)/rtrace: $(SRC)/rtrace_main.cpp $(PKG)/librtpt.so $(HDRS)
 	$(HOSTCXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -lrtpt -Wl,-rpath,'$$ORIGIN'

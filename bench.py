@@ -3,18 +3,23 @@
 
 Metric (BASELINE.json): Msamples/s (pixels x spp) on the Cornell box at 1080p,
 1/2/4/8 MI355X, plus HBM GB/s.  Workload at N=1 = config 2 of BASELINE.json:
-Cornell box (RTrace/scene.swift) 1920x1080, 256 spp, 3 bounces, one step = one
+Cornell box (RTrace/scene.swift) 1920x1080, 256 spp, 3 bounces; one step = one
 full render of the frame on the GPU (the pathTrace dispatch of
 RTrace/renderer.swift:117-146) with inputs resident in HBM.
 
-N>1 (torchrun, one process per GPU, RCCL): weak scaling — every rank renders
-1080/N interleaved rows of the same 1080p frame at 256*N spp (fixed
-1920*1080*256 samples per GPU), then ONE gather of the tiles to rank 0 over
-RCCL; the timed step includes the gather.
+N>1, one process per GPU (launched by torch.distributed.run, or by this script
+itself: `python bench.py --gpus N` spawns its N ranks as child processes before
+anything touches a GPU).  Weak scaling: every rank renders the 1080/N
+interleaved rows y = rank (mod N) of the same 1080p frame at 256*N spp (fixed
+1920*1080*256 samples per GPU); the tiles are gathered to rank 0 by ONE RCCL
+gather inside the C-ABI (rt_comm_init / rt_render_gather, include/rtpt.h) and
+the timed step includes it.  torch.distributed (gloo, CPU) only carries the
+communicator id, the barriers and the max over ranks.
 
 Prints one JSON line on rank 0.  The CPU baseline (rank 0, N=1 only) is the
-scalar C oracle (oracle/liboracle.so, "port") on a bounded sample of the same
-frame, timed on this host's cores.
+scalar C oracle (oracle/liboracle.so, "port") on every core this process may
+use, on a bounded sample of the same frame: rows of the timed image at the
+timed spp, which are also compared bit for bit with the GPU's timed frame.
 """
 from __future__ import annotations
 
@@ -23,6 +28,7 @@ import ctypes
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -33,15 +39,18 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/sec (pixels×spp) Cornell box 1080p at 1/2/4/8 MI355X; HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2  # CUs x SIMDs x clock / 2 cycles per wave64 VALU op
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+# instruction (a 64-lane op issues over 2 cycles on the 32-wide SIMD)
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
 BYTES_PER_PIXEL = 4 + 16       # seed read (u32) + rgba32F store, per launch
 
 
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=150,
+                    help="timed steps (default: ~4 s of GPU time at N=1)")
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scene", default="cornell", choices=["cornell", "spheres", "triangles"])
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -53,8 +62,34 @@ def parse():
     ap.add_argument("--batch-spp", type=int, default=0,
                     help="progressive mode: launches of this many spp into a running sum")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads (default: every CPU this process may use: its "
+                         "affinity, capped by the cgroup CPU quota)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` outside torchrun: start N ranks of this script as child
+    processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), before any GPU call in
+    this process, and return the worst exit status."""
+    import socket
+    import torch
+    have = torch.cuda.device_count()  # counts devices without initialising HIP
+    if have < n:
+        raise SystemExit(f"--gpus {n}: only {have} GPU(s) visible")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def load_profile_json(name):
@@ -67,15 +102,44 @@ def load_profile_json(name):
     return None
 
 
-def cpu_baseline(scene, width, height, bounces, threads, cpu_seconds=10.0):
-    """Scalar C oracle (the identical shader math) on the host cores."""
+def host_cpu():
+    """Cores this process may use and the host CPU model (BASELINE.md asks for
+    nproc and the lscpu model next to every CPU number)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:  # cgroup v2 CPU quota ("max 100000" = none)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "usable_cpus": usable, "model": model}
+
+
+def cpu_baseline(scene, width, height, spp, bounces, threads, seconds, gpu_frame):
+    """Scalar C oracle (the identical shader math) on the host cores, timed on
+    rows y = 0 (mod step) of the same frame at the timed spp, sized to about
+    `seconds`; those rows are then compared with the GPU's timed frame."""
     L = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     L.pto_render.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_void_p, ctypes.c_uint32,
                              ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [ctypes.c_void_p] * 3 + [ctypes.c_int]
     from gpuraytracer_amd import seed_splitmix
     seeds = seed_splitmix(width, height)
 
-    def run(spp, row_step, nthreads):
+    def run(n_spp, row_step, nthreads):
         rows = (height - 1) // row_step + 1
         out = np.empty((rows, width, 4), np.float32)
         ptr = lambda x: ctypes.cast(ctypes.pointer(x), ctypes.c_void_p)  # noqa: E731
@@ -84,36 +148,42 @@ def cpu_baseline(scene, width, height, bounces, threads, cpu_seconds=10.0):
                          ptr(scene.light), ctypes.cast(scene.vertices, ctypes.c_void_p),
                          scene.n_triangles,
                          None if scene.spheres is None else ctypes.cast(scene.spheres, ctypes.c_void_p),
-                         scene.n_spheres, seeds.ctypes.data_as(ctypes.c_void_p), spp, bounces, 0,
+                         scene.n_spheres, seeds.ctypes.data_as(ctypes.c_void_p), n_spp, bounces, 0,
                          0, row_step, 0, None, None, out.ctypes.data_as(ctypes.c_void_p), nthreads)
         dt = time.perf_counter() - t0
         assert r == 0
-        return rows * width * spp / dt / 1e6, rows * width * spp, dt
+        return out, rows * width * n_spp, dt
 
-    def sized(seconds, nthreads):
-        # probe on ever denser row sets until one takes >= 0.3 s, then size the
-        # sample to ~`seconds` of CPU work
-        step = 256
-        while True:
-            rate, _, t = run(1, step, nthreads)
-            if t >= 0.3 or step == 1:
-                break
-            step = max(1, step // 4)
-        want = rate * 1e6 * seconds
-        frame = width * height
-        if want >= frame:
-            spp, step = max(1, int(round(want / frame))), 1
-        else:
-            spp, step = 1, max(1, int(math.ceil(frame / want)))
-        v, n, t = run(spp, step, nthreads)
-        rows = "the full" if step == 1 else f"1 in {step} rows of the"
-        return v, f"{rows} {width}x{height} frame at {spp} spp, {bounces} bounces = {n} samples in {t:.2f} s"
-
-    v_all, s_all = sized(cpu_seconds, threads)
-    v_one, s_one = sized(cpu_seconds / 4, 1)
+    # probe the rate at 1 spp on a sparse row set, then size the timed sample
+    step = 64
+    while True:
+        _, n, t = run(1, step, threads)
+        if t >= 0.3 or step == 1:
+            break
+        step = max(1, step // 4)
+    rate = n / t
+    want_rows = rate * seconds / (width * spp)
+    step = max(1, int(math.ceil(height / max(want_rows, 1.0))))
+    out, n, t = run(spp, step, threads)
+    v_all = n / t / 1e6
+    ref = out
+    got = gpu_frame[::step]
+    same = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
+    # single thread: 1 spp on a sparse row set, ~seconds/4 (the all-thread
+    # probe rate over the threads that could actually run at once)
+    per_thread = rate / max(1, min(threads, host_cpu()["usable_cpus"]))
+    step1 = max(1, int(math.ceil(height / max(per_thread * seconds / 4 / width, 1.0))))
+    _, n1, t1 = run(1, step1, 1)
+    rows = "every row" if step == 1 else f"rows y = 0 (mod {step})"
     return {"value": round(v_all, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{s_all} on {threads} threads (scalar C oracle, -O2)",
-            "single_thread_value": round(v_one, 4), "single_thread_sample": s_one}
+            "sample": (f"{rows} of the {width}x{height} frame at {spp} spp, {bounces} bounces = "
+                       f"{n} samples in {t:.2f} s on {threads} threads (scalar C oracle, -O2)"),
+            "host": host_cpu(),
+            "single_thread_value": round(n1 / t1 / 1e6, 4),
+            "single_thread_sample": (f"rows y = 0 (mod {step1}) at 1 spp = {n1} samples in "
+                                     f"{t1:.2f} s"),
+            "timed_frame_rows_bit_exact_vs_oracle": same,
+            "timed_frame_rows_checked": (height - 1) // step + 1}
 
 
 def main():
@@ -121,20 +191,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run "
-                             "(one process per GPU)")
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
     import torch
     import torch.distributed as dist
 
+    if world > 1:  # CPU plumbing only: comm id, barriers, max over ranks
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
 
-    from gpuraytracer_amd import Renderer, RenderParams, Scene
-    from gpuraytracer_amd.tiles import assemble, rank_rows, tile_rows_max
+    from gpuraytracer_amd import RenderParams, Renderer, Scene, comm_unique_id
 
     W, H = args.width, args.height
     if args.scene == "cornell":
@@ -149,55 +218,60 @@ def main():
         scene = Scene.random_triangles(W, H, args.triangles, seed=7)
         workload = f"triangles{args.triangles}_{W}x{H}_{args.spp}spp_b{args.bounces}"
     renderer = Renderer(scene, device=local)
-    row_start, row_step, rows = rank_rows(H, world, rank)
+    if world > 1:
+        ids = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        renderer.comm_init(rank, world, ids[0])
     spp = args.spp * world  # weak scaling: W*H*spp samples per GPU whatever N
-    rows_max = tile_rows_max(H, world)
-    tile = torch.empty((rows_max, W, 4), dtype=torch.float32, device=device)
-    params = RenderParams(spp=spp, bounces=args.bounces, row_start=row_start, row_step=row_step,
-                          row_count=rows)
-    gathered = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    rows = (H - 1 - rank) // world + 1 if rank < H else 0  # this rank's interleaved rows
+    frame = torch.empty((H, W, 4), dtype=torch.float32, device=device) if rank == 0 else None
+    params = RenderParams(spp=spp, bounces=args.bounces)
     stream = torch.cuda.current_stream()
 
     def step(evs=None):
         if evs is not None:
             evs[0].record(stream)
         if args.batch_spp:
-            renderer.render_progressive(params, args.batch_spp, out=tile, stream=stream)
+            renderer.render_progressive(params, args.batch_spp, out=frame, stream=stream,
+                                        gather=world > 1)
+        elif world > 1:
+            renderer.render_gather(params, out=frame, stream=stream)
         else:
-            renderer.render(params, out=tile, stream=stream)
+            renderer.render(params, out=frame, stream=stream)
         if evs is not None:
             evs[1].record(stream)
+
+    def barrier():
+        torch.cuda.synchronize()
         if world > 1:
-            dist.gather(tile, gathered, dst=0)
+            dist.barrier()
 
     for _ in range(args.warmup):
         step()
+    launch = renderer.last_launch()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    # HIP events on the stream the kernel runs on, around every timed step: at
+    # N = 1 a step is exactly one kernel launch (or the launches of one
+    # progressive frame); at N > 1 it also holds the gather, and the kernel
+    # alone is the last launch's own events (rt_last_kernel_ms)
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kernel_ms = step_ms if world == 1 else renderer.last_kernel_ms()
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kernel_ms, step_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms_max = float(t[0]), float(t[1])
+        elapsed, kernel_ms_max, step_ms_max = (float(v) for v in t)
     else:
-        kernel_ms_max = kernel_ms
+        kernel_ms_max, step_ms_max = kernel_ms, step_ms
 
-    frame_ok = True
     if rank == 0:
-        frame = assemble(gathered, H) if world > 1 else tile[:rows]
         frame_ok = bool(torch.isfinite(frame).all().item()) and bool((frame[..., 3] == 1).all().item())
-
-    if rank == 0:
         total_samples = W * H * spp * args.steps  # all ranks together
         value = total_samples / elapsed / 1e6
         launch_bytes = W * rows * BYTES_PER_PIXEL
@@ -206,7 +280,8 @@ def main():
             # (+ sum read), last 52 B/px (+ frame store) — SURVEY §8d
             nb = -(-spp // args.batch_spp)
             launch_bytes = W * rows * (20 + 36 * (nb - 2) + 52)
-        achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+        kernel_s = kernel_ms * 1e-3
+        achieved = launch_bytes / kernel_s / 1e9
         traffic = None
         prof = load_profile_json("pmc_summary.json")
         compute = None
@@ -215,11 +290,14 @@ def main():
                 and prof.get("kernel_src_sha") == kernel_source_sha()):
             traffic = prof.get("hbm_bytes_per_launch")
             if prof.get("sq_insts_valu_per_launch"):
-                wi = prof["sq_insts_valu_per_launch"] / (kernel_ms * 1e-3)
+                wi = prof["sq_insts_valu_per_launch"] / kernel_s
                 compute = {"bound": "valu", "achieved": round(wi / 1e9, 2),
                            "peak": round(VALU_PEAK_WAVE_INSTR / 1e9, 2),
                            "unit": "G wave64-VALU-instr/s", "frac": round(wi / VALU_PEAK_WAVE_INSTR, 4),
-                           "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) / live kernel time"}
+                           "peak_derivation": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 "
+                                              "VALU instruction",
+                           "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json, same "
+                                     "kernel_src_sha) / live kernel time"}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -240,26 +318,30 @@ def main():
                      "Cornell room, splitmix64 seeds"),
             "config": {"workload": workload, "width": W, "height": H, "spp_per_gpu": args.spp,
                        "spp_frame": spp, "bounces": args.bounces,
-                       "parallelism": (f"{world} row-interleaved tiles + 1 RCCL gather" if world > 1
-                                       else "single GPU")},
+                       "parallelism": (f"{world} row-interleaved tiles + 1 RCCL gather "
+                                       "(rt_render_gather)" if world > 1 else "single GPU")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "path_trace_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": launch["kernel"], "kernel_ms": round(kernel_s * 1e3, 4),
                          "algorithmic_bytes_per_launch": launch_bytes},
             "compute_roofline": compute,
+            "launch": launch,
+            "step_ms_events": round(step_ms, 4),
             "kernel_ms_max_rank": round(kernel_ms_max, 4),
+            "step_ms_max_rank": round(step_ms_max, 4),
             "frame_ok": frame_ok,
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline != "off":
-            try:
-                aff = len(os.sched_getaffinity(0))
-            except AttributeError:
-                aff = os.cpu_count() or 1
-            threads = args.cpu_threads or max(1, min(16, aff))
-            out["cpu_baseline"] = cpu_baseline(scene, W, H, args.bounces, threads)
+            # every CPU this process may run on at once: the affinity mask,
+            # capped by the cgroup CPU quota (oversubscribing a 16-CPU quota
+            # with 256 threads measured 13.2 instead of 22.3 Msamples/s)
+            threads = args.cpu_threads or host_cpu()["usable_cpus"]
+            out["cpu_baseline"] = cpu_baseline(scene, W, H, spp, args.bounces, threads,
+                                               args.cpu_seconds, frame.cpu().numpy())
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
     renderer.close()
 

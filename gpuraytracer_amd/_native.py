@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTPT_LIB overrides the in-tree library (A/B builds of the kernel).
 library_path = os.environ.get("RTPT_LIB") or os.path.join(_HERE, "librtpt.so")
@@ -92,10 +92,22 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
 
 
 RT_OK = 0
-RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE, RT_KEEP_SUM = 0x1, 0x2, 0x4, 0x8
+RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE, RT_KEEP_SUM, RT_OUT_RGBA8 = 0x1, 0x2, 0x4, 0x8, 0x10
 RT_MAX_BOUNCES = 4
+RT_COMM_ID_BYTES = 128
 STATUS = {0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_NO_DEVICE", 3: "RT_ERR_OUT_OF_MEMORY",
           4: "RT_ERR_LAUNCH", 5: "RT_ERR_STATE", 6: "RT_ERR_COMM"}
+
+class LaunchInfo(ctypes.Structure):  # rt_launch_info
+    _fields_ = [("kernel", ctypes.c_char * 96)] + [(n, ctypes.c_uint32) for n in
+                ("lanes_per_pixel", "halton_tables", "small_index", "block_threads", "grid_x",
+                 "grid_y", "lds_bytes")]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["kernel"] = self.kernel.decode()
+        return d
+
 
 class MisParamsC(ctypes.Structure):  # rt_mis_params
     _fields_ = [(n, ctypes.c_uint32) for n in
@@ -112,6 +124,11 @@ SIGNATURES = {
     "rt_render_async": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),
     "rt_last_kernel_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_destroy": (ctypes.c_int, [_P]),
+    "rt_last_launch": (ctypes.c_int, [_P, ctypes.POINTER(LaunchInfo)]),
+    "rt_comm_unique_id": (ctypes.c_int, [_P]),
+    "rt_comm_init": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P]),
+    "rt_render_gather": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),
+    "rt_build_sha": (ctypes.c_char_p, []),
     "rt_debug_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "rt_last_error": (ctypes.c_char_p, [_P]),
     "rt_status_string": (ctypes.c_char_p, [ctypes.c_int]),
@@ -188,6 +205,12 @@ def _load():
         fn.argtypes = args
     if handle.rt_abi_version() != ABI_VERSION:
         raise ImportError(f"librtpt.so ABI {handle.rt_abi_version()} != {ABI_VERSION}")
+    if not os.environ.get("RTPT_LIB"):  # A/B builds (RTPT_LIB) are checked by their maker
+        from .srchash import kernel_source_sha
+        built, tree = handle.rt_build_sha().decode(), kernel_source_sha()
+        if built != tree:
+            raise ImportError(f"{library_path} was built from other sources (hash {built}, "
+                              f"tree {tree}): rebuild it with `make`")
     return handle
 
 

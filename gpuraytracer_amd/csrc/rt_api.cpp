@@ -7,6 +7,7 @@
 // owns every device buffer, and every failure is returned as an rt_status with
 // a message (the reference fatalError()s / force-unwraps instead).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -50,11 +51,20 @@ struct rt_ctx {
     float4* d_sum = nullptr;
     size_t sum_cap = 0;  // pixels
     bool sum_valid = false;
-    uint32_t sum_row_start = 0, sum_row_step = 0, sum_row_count = 0, sum_samples = 0;
+    uint32_t sum_row_start = 0, sum_row_step = 0, sum_row_count = 0;
+    uint32_t sum_first = 0, sum_samples = 0;  // the sum holds samples [first, first + samples)
     void* d_out = nullptr;  // staging for host outputs
     size_t out_cap = 0;     // bytes
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    rt::LaunchInfo launch{};  // what the last rt_render launched (rt_last_launch)
+    bool launched = false;
+    ncclComm_t comm = nullptr;  // rt_comm_init: row-tile gather over RCCL
+    int rank = 0, world = 1;
+    void* d_tile = nullptr;     // this rank's rows before the gather
+    size_t tile_cap = 0;
+    void* d_gather = nullptr;   // rank 0: world x rows_max x W pixels
+    size_t gather_cap = 0;
     uint32_t lanes = 0;  // RTPT_LANES=1|4|16: lanes per pixel (tuning knob; 0 = auto)
     rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|pairsmem|sorted|bvh (tuning knob)
     std::string err;
@@ -122,6 +132,9 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_seeds);
     (void)hipFree(c->d_sum);
     (void)hipFree(c->d_out);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    (void)hipFree(c->d_tile);
+    (void)hipFree(c->d_gather);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -154,18 +167,21 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     if (want_out && !out) return fail(c, RT_ERR_INVALID_ARG, "out is null");
     if (p->accumulate) {
         if (!c->sum_valid || c->sum_row_start != start || c->sum_row_step != step ||
-            c->sum_row_count != count || c->sum_samples != p->sample_base)
+            c->sum_row_count != count ||
+            (uint64_t)c->sum_first + c->sum_samples != (uint64_t)p->sample_base)
             return fail(c, RT_ERR_STATE,
-                        "accumulate: context sum does not hold samples [0, sample_base) of "
-                        "these rows (render with RT_KEEP_SUM first)");
+                        "accumulate: context sum does not end at sample_base for these rows "
+                        "(render with RT_KEEP_SUM first)");
     }
-    const uint64_t total = (uint64_t)(p->accumulate ? p->sample_base : 0u) + p->spp;
+    const uint64_t total = (uint64_t)(p->accumulate ? c->sum_samples : 0u) + p->spp;
     if (total == 0 || total > 0xFFFFFFFFull)
         return fail(c, RT_ERR_INVALID_ARG, "samples in the sum must be in [1, 2^32)");
 
     const size_t W = (size_t)c->scene.cam.W;
     const size_t pixels = (size_t)count * W;
-    const size_t px_bytes = (p->flags & RT_OUT_FP16) ? 8u : 16u;
+    if ((p->flags & RT_OUT_FP16) && (p->flags & RT_OUT_RGBA8))
+        return fail(c, RT_ERR_INVALID_ARG, "RT_OUT_FP16 and RT_OUT_RGBA8 are exclusive");
+    const size_t px_bytes = (p->flags & RT_OUT_RGBA8) ? 4u : (p->flags & RT_OUT_FP16) ? 8u : 16u;
     hipError_t e;
     if (keep_sum || p->accumulate) {
         if (c->sum_cap < pixels) {
@@ -238,7 +254,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.row_count = count;
     K.accumulate = p->accumulate ? 1u : 0u;
     K.samples_total = (uint32_t)total;
-    K.flags = (p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u;
+    K.flags = ((p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u) | ((p->flags & RT_OUT_RGBA8) ? rt::kOutRgba8 : 0u);
     K.lanes = c->lanes;
     {
         const uint64_t imax = (uint64_t)c->seed_max + p->sample_base + (p->spp ? p->spp - 1u : 0u);
@@ -247,8 +263,9 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
 
     if (keep_sum && !p->accumulate) c->sum_valid = false;  // being overwritten
     (void)hipEventRecord(c->ev0, stream);
-    e = rt::launch_path_trace(K, p->bounces, c->scene_mem, stream);
+    e = rt::launch_path_trace(K, p->bounces, c->scene_mem, stream, &c->launch);
     if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "path_trace launch", e);
+    c->launched = true;
     (void)hipEventRecord(c->ev1, stream);
     c->timed = true;
     if (keep_sum || p->accumulate) {  // the kernel (re)wrote the running sums
@@ -256,6 +273,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
         c->sum_row_start = start;
         c->sum_row_step = step;
         c->sum_row_count = count;
+        if (!p->accumulate) c->sum_first = p->sample_base;
         c->sum_samples = (uint32_t)total;
     }
     if (want_out && !out_is_device) {
@@ -266,6 +284,70 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     if (sync) {
         if ((e = hipStreamSynchronize(stream)) != hipSuccess)
             return hip_fail(c, RT_ERR_LAUNCH, "path_trace execution", e);
+    }
+    return RT_OK;
+}
+
+int ensure_staging(rt_ctx* c, void** buf, size_t* cap, size_t bytes, const char* what);
+
+int nccl_fail(rt_ctx* ctx, const char* what, ncclResult_t r) {
+    return fail(ctx, RT_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+size_t pixel_bytes(uint32_t flags) {
+    return (flags & RT_OUT_RGBA8) ? 4u : (flags & RT_OUT_FP16) ? 8u : 16u;
+}
+
+// rt_render_gather: this rank's interleaved rows into d_tile, one ncclGather of
+// the (padded, equal-sized) tiles to rank 0, then one strided copy per rank
+// that puts tile row j of rank k at frame row k + j*world.
+int render_gather_impl(rt_ctx* c, const rt_render_params* p, void* frame, hipStream_t stream) {
+    if (!p) return fail(c, RT_ERR_INVALID_ARG, "params is null");
+    if (!c->comm) return fail(c, RT_ERR_STATE, "no communicator (rt_comm_init)");
+    if (p->row_start || p->row_step > 1 || p->row_count)
+        return fail(c, RT_ERR_INVALID_ARG, "rt_render_gather partitions the rows itself: "
+                                           "params must name the whole frame (row_start 0, "
+                                           "row_step 0 or 1, row_count 0)");
+    const bool want_out = !(p->flags & RT_OUT_NONE);
+    const bool dev = (p->flags & RT_OUT_DEVICE) != 0;
+    if (want_out && c->rank == 0 && !frame) return fail(c, RT_ERR_INVALID_ARG, "frame is null on rank 0");
+    const uint32_t H = (uint32_t)c->scene.cam.H, W = (uint32_t)c->scene.cam.W, N = (uint32_t)c->world;
+    const uint32_t rows_max = (H + N - 1) / N;
+    const uint32_t mine = (uint32_t)c->rank < H ? (H - 1u - (uint32_t)c->rank) / N + 1u : 0u;
+    const size_t px = pixel_bytes(p->flags);
+    const size_t tile_bytes = (size_t)rows_max * W * px;
+    int st;
+    if (want_out && (st = ensure_staging(c, &c->d_tile, &c->tile_cap, tile_bytes, "hipMalloc(tile)")) != RT_OK)
+        return st;
+    if (mine > 0) {  // a rank past the last row renders nothing but still joins the gather
+        rt_render_params q = *p;
+        q.row_start = (uint32_t)c->rank;
+        q.row_step = N;
+        q.row_count = mine;
+        q.flags = p->flags | RT_OUT_DEVICE;
+        if ((st = render_impl(c, &q, c->d_tile, true, stream, false)) != RT_OK) return st;
+    }
+    if (!want_out) return RT_OK;
+    if (c->rank == 0 && (st = ensure_staging(c, &c->d_gather, &c->gather_cap, tile_bytes * N,
+                                             "hipMalloc(gather)")) != RT_OK)
+        return st;
+    ncclResult_t r = ncclGather(c->d_tile, c->rank == 0 ? c->d_gather : nullptr, tile_bytes, ncclUint8,
+                                0, c->comm, stream);
+    if (r != ncclSuccess) return nccl_fail(c, "ncclGather", r);
+    if (c->rank == 0) {
+        const size_t row = (size_t)W * px;
+        for (uint32_t k = 0; k < N && k < H; ++k) {
+            const uint32_t rows_k = (H - 1u - k) / N + 1u;
+            hipError_t e = hipMemcpy2DAsync(static_cast<char*>(frame) + k * row, N * row,
+                                            static_cast<char*>(c->d_gather) + k * tile_bytes, row,
+                                            row, rows_k,
+                                            dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, stream);
+            if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpy2DAsync(frame rows)", e);
+        }
+    }
+    if (!dev) {
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail(c, RT_ERR_COMM, "render+gather execution", e);
     }
     return RT_OK;
 }
@@ -589,6 +671,63 @@ int rt_last_kernel_ms(rt_ctx* c, float* ms) {
     if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "hipEventElapsedTime", e);
     return RT_OK;
 }
+
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]) {
+    if (!id) return fail(nullptr, RT_ERR_INVALID_ARG, "id is null");
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return nccl_fail(nullptr, "ncclGetUniqueId", r);
+    memcpy(id, &u, sizeof(u));
+    return RT_OK;
+}
+
+int rt_comm_init(rt_ctx* c, int32_t rank, int32_t world, const uint8_t id[RT_COMM_ID_BYTES]) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    if (!id) return fail(c, RT_ERR_INVALID_ARG, "id is null");
+    if (world < 1 || rank < 0 || rank >= world)
+        return fail(c, RT_ERR_INVALID_ARG, "need 0 <= rank < world");
+    if (c->comm) return fail(c, RT_ERR_STATE, "context already has a communicator");
+    DeviceGuard g(c->device);
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, world, u, rank);
+    if (r != ncclSuccess) return nccl_fail(c, "ncclCommInitRank", r);
+    c->comm = comm;
+    c->rank = rank;
+    c->world = world;
+    return RT_OK;
+}
+
+int rt_render_gather(rt_ctx* c, const rt_render_params* p, void* frame, void* hip_stream) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    DeviceGuard g(c->device);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    return render_gather_impl(c, p, frame, s);
+}
+
+int rt_last_launch(const rt_ctx* c, rt_launch_info* info) {
+    if (!c || !info) return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->launched) return RT_ERR_STATE;
+    memset(info, 0, sizeof(*info));
+    static_assert(sizeof(info->kernel) == sizeof(c->launch.kernel), "kernel name buffer");
+    memcpy(info->kernel, c->launch.kernel, sizeof(info->kernel));
+    info->kernel[sizeof(info->kernel) - 1] = 0;
+    info->lanes_per_pixel = c->launch.lanes;
+    info->halton_tables = c->launch.tables;
+    info->small_index = c->launch.small;
+    info->block_threads = c->launch.threads;
+    info->grid_x = c->launch.grid_x;
+    info->grid_y = c->launch.grid_y;
+    info->lds_bytes = c->launch.lds;
+    return RT_OK;
+}
+
+#ifndef RT_SRC_SHA
+#define RT_SRC_SHA "unknown"
+#endif
+const char* rt_build_sha(void) { return RT_SRC_SHA; }
 
 int rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;

@@ -1,12 +1,14 @@
 // rt_image.cpp — the reference's image epilogue (RTrace/image.swift:15-100):
 // the rgba16Float render texture read back as Float16 (:35-38), then per RGB
 // channel x2 exposure, Reinhard v/(v+1), pow(v, 1/2.2), clamp to [0,1] and a
-// truncating UInt8(v*255) (:41-60); alpha 255 (:63).  Host-side, like the
-// reference (a scalar CPU loop there too).
+// truncating UInt8(v*255) (:41-60); alpha 255 (:63).  Host-side form of the
+// RT_OUT_RGBA8 epilogue the kernel fuses into its store: both call
+// rt::tonemap_channel (rt_math.h), so the bytes are identical.
 #include <math.h>
 #include <string.h>
 
 #include "../../include/rtpt.h"
+#include "rt_math.h"
 
 namespace {
 
@@ -62,17 +64,9 @@ float from_half(uint16_t h) {
 
 extern "C" void rt_tonemap_rgba8(const float* in, size_t n, uint8_t* out) {
     if (!in || !out) return;
-    const float exposure = 2.0f;  // image.swift:41
-    const float gamma = 2.2f;     // image.swift:42
     for (size_t i = 0; i < n; ++i) {
-        for (int ch = 0; ch < 3; ++ch) {
-            float v = from_half(to_half(in[4 * i + ch]));
-            v *= exposure;
-            v = v / (v + 1.0f);
-            v = powf(v, 1.0f / gamma);
-            v = fmaxf(0.0f, fminf(1.0f, v));
-            out[4 * i + ch] = (uint8_t)(v * 255.0f);
-        }
+        for (int ch = 0; ch < 3; ++ch)
+            out[4 * i + ch] = rt::tonemap_channel(from_half(to_half(in[4 * i + ch])));
         out[4 * i + 3] = 255;
     }
 }

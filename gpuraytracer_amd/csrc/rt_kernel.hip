@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <stdio.h>
+
 #include "rt_kernel.hpp"
 #include "rt_halton.hpp"
 #include "rt_trace.hpp"
@@ -168,6 +170,28 @@ __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv
     }
 }
 
+// The pixel store (raytrace.metal:109): float4(luminance, 1) as rgba32F, as
+// the reference's rgba16F texture (renderer.swift:74-82), or that texture
+// tonemapped to the reference's 8-bit image (RTrace/image.swift:35-65: fp16
+// read-back, then rt::tonemap_channel) -- 16, 8 or 4 bytes, one store.
+__device__ __forceinline__ void store_pixel(const KParams& P, size_t o, float r, float g, float b) {
+    if (P.flags & kOutRgba8) {
+        const uint8_t cr = tonemap_channel(__half2float(__float2half_rn(r)));
+        const uint8_t cg = tonemap_channel(__half2float(__float2half_rn(g)));
+        const uint8_t cb = tonemap_channel(__half2float(__float2half_rn(b)));
+        reinterpret_cast<uchar4*>(P.out)[o] = make_uchar4(cr, cg, cb, 255);
+    } else if (P.flags & kOutFp16) {
+        ushort4 h;
+        h.x = __half_as_ushort(__float2half_rn(r));
+        h.y = __half_as_ushort(__float2half_rn(g));
+        h.z = __half_as_ushort(__float2half_rn(b));
+        h.w = __half_as_ushort(__float2half_rn(1.0f));
+        reinterpret_cast<ushort4*>(P.out)[o] = h;
+    } else {
+        reinterpret_cast<float4*>(P.out)[o] = make_float4(r, g, b, 1.0f);
+    }
+}
+
 // ---- sorted-path variant ----------------------------------------------------
 // Between bounces the 256 paths of a workgroup are counting-sorted through LDS
 // by the octant of their next direction, dead paths last (9 buckets).  Waves
@@ -296,6 +320,13 @@ size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 #define RT_MIN_WAVES_PER_EU_SPH 8
 #endif
 constexpr uint32_t kHaltonTabMinRounds = 8;  // samples per lane below which no tables
+// Whether a launch fills the LDS low-digit Halton tables: box-cluster kernel,
+// fixed-digit indices, and every lane tracing enough samples to amortise the
+// fill (~700 VALU per thread): config 1 (1 spp) runs without them.  The kernel
+// and the launcher's rt_last_launch report share this one definition.
+__host__ __device__ constexpr bool halton_tables_on(int geo, bool small, uint32_t spp, uint32_t L) {
+    return geo == kGeoPairClu && small && (spp + L - 1) / L >= kHaltonTabMinRounds;
+}
 #ifndef RT_MIN_WAVES_PER_EU_CLU
 // box-cluster kernel: 7 waves/SIMD runs as fast as 8 and spills 6 VGPRs
 // instead of 30 (HBM traffic 146 MB instead of 19 GB per 1080p launch)
@@ -345,9 +376,7 @@ void path_trace_kernel(KParams P) {
         }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
-            // tables only when every lane traces enough samples to amortise the
-            // fill (~700 VALU per thread): config 1 (1 spp) runs without them
-            const bool tab = SMALL && (P.spp + L - 1) / L >= kHaltonTabMinRounds;
+            const bool tab = halton_tables_on(GEO, SMALL, P.spp, L);
             sv.htab = tab ? reinterpret_cast<const float*>(lds + ng4 + kCluF4 * P.nC) : nullptr;
             if (tab)
                 fill_halton_tables(reinterpret_cast<float*>(lds + ng4 + kCluF4 * P.nC), threadIdx.x,
@@ -448,16 +477,7 @@ void path_trace_kernel(KParams P) {
     if (P.out) {
         const float fs = (float)P.samples_total;                 // :106
         const float r = lum.x / fs, g = lum.y / fs, bl = lum.z / fs;
-        if (P.flags & kOutFp16) {                                // rgba16Float texture
-            ushort4 h;
-            h.x = __half_as_ushort(__float2half_rn(r));
-            h.y = __half_as_ushort(__float2half_rn(g));
-            h.z = __half_as_ushort(__float2half_rn(bl));
-            h.w = __half_as_ushort(__float2half_rn(1.0f));
-            reinterpret_cast<ushort4*>(P.out)[o] = h;
-        } else {
-            reinterpret_cast<float4*>(P.out)[o] = make_float4(r, g, bl, 1.0f);  // :109
-        }
+        store_pixel(P, o, r, g, bl);
     }
 }
 
@@ -525,16 +545,7 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace
     if (P.out) {
         const float fs = (float)P.samples_total;                 // :106
         const float r = lum.x / fs, g = lum.y / fs, bl = lum.z / fs;
-        if (P.flags & kOutFp16) {
-            ushort4 h;
-            h.x = __half_as_ushort(__float2half_rn(r));
-            h.y = __half_as_ushort(__float2half_rn(g));
-            h.z = __half_as_ushort(__float2half_rn(bl));
-            h.w = __half_as_ushort(__float2half_rn(1.0f));
-            reinterpret_cast<ushort4*>(P.out)[o] = h;
-        } else {
-            reinterpret_cast<float4*>(P.out)[o] = make_float4(r, g, bl, 1.0f);  // :109
-        }
+        store_pixel(P, o, r, g, bl);
     }
 }
 
@@ -563,6 +574,25 @@ inline int lanes_per_pixel(const KParams& P) {
     return P.spp >= 4 ? 4 : 1;
 }
 
+constexpr int kGeoPairSorted = 3;  // pair records + per-bounce octant sort of the paths
+
+// The most recent launch of this thread (launch_path_trace copies it out).
+thread_local LaunchInfo g_last;
+
+template <int B, int GEO, bool SPH, bool SMALL, int L>
+void note_launch(const char* name, const KParams& P, dim3 grid, uint32_t threads, size_t lds) {
+    LaunchInfo& I = g_last;
+    snprintf(I.kernel, sizeof(I.kernel), "rt::%s<%d, %d, %s, %s, %d>", name, B, GEO,
+             SPH ? "true" : "false", SMALL ? "true" : "false", L);
+    I.lanes = (uint32_t)L;
+    I.tables = halton_tables_on(GEO, SMALL, P.spp, (uint32_t)L) ? 1u : 0u;
+    I.small = SMALL ? 1u : 0u;
+    I.threads = threads;
+    I.grid_x = grid.x;
+    I.grid_y = grid.y;
+    I.lds = (uint32_t)lds;
+}
+
 // Dynamic LDS above 64 KB must be allowed per kernel (the compact sphere BVH).
 inline hipError_t allow_lds(const void* kernel, size_t bytes) {
     if (bytes <= 65536) return hipSuccess;
@@ -583,9 +613,10 @@ hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
         const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL, L>, lds_bytes);
         if (e != hipSuccess) return e;
     }
+    const size_t lds = (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes;
+    note_launch<B, GEO, SPH, SMALL, L>("path_trace_kernel", Q, grid, block_threads(GEO), lds);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL, L>), grid, dim3(block_threads(GEO)),
-                       (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,
-                       stream, Q);
+                       lds, stream, Q);
     return hipGetLastError();
 }
 
@@ -602,9 +633,10 @@ hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
         const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL>, lds_bytes);
         if (e != hipSuccess) return e;
     }
+    const size_t lds = (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes;
+    note_launch<B, GEO, SPH, SMALL, 1>("path_trace_kernel", P, grid, block_threads(GEO), lds);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(block_threads(GEO)),
-                       (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes,
-                       stream, P);
+                       lds, stream, P);
     return hipGetLastError();
 }
 
@@ -627,12 +659,12 @@ hipError_t launch_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
 template <int B, bool SPH, bool SMALL>
 hipError_t launch_sorted_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
+    note_launch<B, kGeoPairSorted, SPH, SMALL, 1>("path_trace_sorted_kernel", P, grid, kBlockThreads,
+                                                   lds_bytes);
     hipLaunchKernelGGL((path_trace_sorted_kernel<B, SPH, SMALL>), grid, dim3(kBlockThreads),
                        lds_bytes, stream, P);
     return hipGetLastError();
 }
-
-constexpr int kGeoPairSorted = 3;  // pair records + per-bounce octant sort of the paths
 
 template <int B>
 hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t stream) {
@@ -665,8 +697,9 @@ size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32
     return (size_t)geo4 * sizeof(float4);
 }
 
-hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
-                             hipStream_t stream) {
+namespace {
+hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem mem,
+                                  hipStream_t stream) {
     const bool pairs = P.nP > 0 && mem != SceneMem::kLdsSingle;
     const size_t lds_bytes = kernel_lds_bytes(P.nT, pairs ? P.nP : 0u, P.nS, P.nN);
     int geo = kGeoTriGlobal;
@@ -706,6 +739,15 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
         default: return hipErrorInvalidValue;
     }
 }
+}  // namespace
+
+hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
+                             hipStream_t stream, LaunchInfo* info) {
+    const hipError_t e = launch_path_trace_impl(P, bounces, mem, stream);
+    if (info) *info = g_last;
+    return e;
+}
+
 
 hipError_t read_debug_stats(unsigned long long* out, int n) {
 #ifdef RT_STATS

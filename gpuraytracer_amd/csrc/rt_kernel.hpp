@@ -13,6 +13,7 @@ constexpr uint32_t kBlockThreads = 256;  // 4 waves; each wave = 8x8 pixel tile
 constexpr uint32_t kTile = 16;           // workgroup = 16x16 pixels
 constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
+constexpr uint32_t kOutRgba8 = 0x10u;  // fused image.swift:35-65 epilogue, uchar4 store
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
 // dynamic LDS of the sphere-BVH-in-LDS kernel: two 1024-thread workgroups per
 // CU share 160 KB with their static per-pixel sums (3 KB at 4 lanes per pixel)
@@ -59,9 +60,15 @@ struct KParams {
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);
+// What launch_path_trace launched (rt_last_launch, include/rtpt.h).
+struct LaunchInfo {
+    char kernel[96];
+    uint32_t lanes, tables, small, threads, grid_x, grid_y, lds;
+};
 // Where the workgroup reads the intersection records from.
 enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5, kPairLds = 6 };
-hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream);
+hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream,
+                             LaunchInfo* info);
 hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
 // Arguments of the MIS integrator kernel (rt_mis.hip; Sources/gpuRaytracer/
 // shaders.metal:635-707).

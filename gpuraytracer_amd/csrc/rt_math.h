@@ -151,4 +151,17 @@ RT_HD float pow_pt(float x, float y) {
     return exp_pt(y * log_pt(x));
 }
 
+// One RGB channel of the reference's image epilogue (RTrace/image.swift:41-60)
+// on a value already round-tripped through the rgba16F texture (:35-38):
+// x2 exposure, Reinhard, pow(v, 1/2.2), clamp, truncating UInt8.  The pow is
+// the portable pow_pt; a NaN (an fp16 inf after Reinhard)
+// skips it and clamps to 1, as Swift's min(1.0, NaN) returns 1.0.
+RT_HD uint8_t tonemap_channel(float v) {
+    v = v * 2.0f;                                   // exposure :41,54
+    v = v / (v + 1.0f);                             // Reinhard :55
+    if (v == v) v = pow_pt(v, 1.0f / 2.2f);         // gamma :42,56
+    v = fmaxf(0.0f, fminf(1.0f, v));                // :59
+    return (uint8_t)(v * 255.0f);                   // UInt8(value * 255) :60
+}
+
 }  // namespace rt

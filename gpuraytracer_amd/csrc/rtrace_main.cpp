@@ -153,9 +153,15 @@ class Renderer {
     }
     ~Renderer() { rt_destroy(ctx_); }
 
-    // Renderer.draw() (:117-146); returns kernel seconds
-    double draw(std::vector<float>* image) {
-        image->assign((size_t)opt_.width * opt_.height * 4, 0.0f);
+    // Renderer.draw() (:117-146) followed by saveTextureToImage's tonemap
+    // (image.swift:35-65): with rgba8 the kernel stores the 8-bit image itself
+    // (RT_OUT_RGBA8, the epilogue fused into its store); otherwise the fp32
+    // frame.  Returns kernel seconds.
+    double draw(std::vector<float>* image, std::vector<uint8_t>* rgba8 = nullptr) {
+        const size_t px = (size_t)opt_.width * opt_.height;
+        if (rgba8) rgba8->assign(4 * px, 0);
+        else image->assign(4 * px, 0.0f);
+        void* out = rgba8 ? (void*)rgba8->data() : (void*)image->data();
         const uint32_t batch = opt_.batch ? opt_.batch : opt_.spp;
         double kernel_s = 0.0;
         for (uint32_t base = 0; base < opt_.spp; base += batch) {
@@ -166,8 +172,8 @@ class Renderer {
             p.sample_base = base;
             p.accumulate = base > 0;
             const bool last = base + p.spp >= opt_.spp;
-            p.flags = (last ? 0u : RT_OUT_NONE) | (opt_.batch ? RT_KEEP_SUM : 0u);
-            check(rt_render(ctx_, &p, last ? image->data() : nullptr), ctx_);
+            p.flags = (last ? (rgba8 ? RT_OUT_RGBA8 : 0u) : RT_OUT_NONE) | (opt_.batch ? RT_KEEP_SUM : 0u);
+            check(rt_render(ctx_, &p, last ? out : nullptr), ctx_);
             float ms = 0;
             check(rt_last_kernel_ms(ctx_, &ms), ctx_);
             kernel_s += ms * 1e-3;
@@ -252,12 +258,17 @@ int main(int argc, char** argv) {
                o.width, o.height, o.camera_rays, o.mis_samples, ks);
         return 0;
     }
+    // The PNG is the kernel's fused RGBA8 store; with --pfm the fp32 frame is
+    // kept and tonemapped on the host instead (rt_tonemap_rgba8: same bytes).
     std::vector<float> img;
+    std::vector<uint8_t> rgba8;
     const auto t0 = std::chrono::steady_clock::now();
-    const double ks = r.draw(&img);
+    const double ks = pfm.empty() ? r.draw(&img, &rgba8) : r.draw(&img);
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    std::vector<uint8_t> rgba8((size_t)o.width * o.height * 4);
-    rt_tonemap_rgba8(img.data(), (size_t)o.width * o.height, rgba8.data());
+    if (!pfm.empty()) {
+        rgba8.resize((size_t)o.width * o.height * 4);
+        rt_tonemap_rgba8(img.data(), (size_t)o.width * o.height, rgba8.data());
+    }
     if (!write_png(out.c_str(), rgba8.data(), o.width, o.height)) {
         fprintf(stderr, "failed to write %s\n", out.c_str());
         return 1;

@@ -17,9 +17,10 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._native import (RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE,
-                      CameraGPU, MaterialGPU, MisParamsC, RenderParamsC, RtError, SceneDesc,
-                      SceneInfo, SphereGPU, SquareLightGPU, float3, lib)
+from ._native import (RT_COMM_ID_BYTES, RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16,
+                      RT_OUT_NONE, RT_OUT_RGBA8,
+                      CameraGPU, LaunchInfo, MaterialGPU, MisParamsC, RenderParamsC, RtError,
+                      SceneDesc, SceneInfo, SphereGPU, SquareLightGPU, float3, lib)
 
 DEFAULT_SEED_KEY = 0x5EED00000000
 
@@ -47,6 +48,13 @@ def tonemap_rgba8(rgba32f: np.ndarray) -> np.ndarray:
     lib.rt_tonemap_rgba8(a.ctypes.data_as(ctypes.c_void_p), n,
                          out.ctypes.data_as(ctypes.c_void_p))
     return out
+
+
+def comm_unique_id() -> bytes:
+    """rt_comm_unique_id: the RCCL communicator id rank 0 hands to every rank."""
+    buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)()
+    _check(lib.rt_comm_unique_id(buf))
+    return bytes(buf)
 
 
 class Scene:
@@ -208,13 +216,15 @@ class RenderParams:
     accumulate: bool = False
     keep_sum: bool = False
     fp16: bool = False
+    rgba8: bool = False     # the fused image.swift:35-65 epilogue (RT_OUT_RGBA8)
 
     def c(self, flags: int = 0) -> RenderParamsC:
         p = RenderParamsC()
         p.spp, p.bounces, p.sample_base = self.spp, self.bounces, self.sample_base
         p.row_start, p.row_step, p.row_count = self.row_start, self.row_step, self.row_count
         p.accumulate = 1 if self.accumulate else 0
-        p.flags = flags | (RT_KEEP_SUM if self.keep_sum else 0) | (RT_OUT_FP16 if self.fp16 else 0)
+        p.flags = (flags | (RT_KEEP_SUM if self.keep_sum else 0) | (RT_OUT_FP16 if self.fp16 else 0)
+                   | (RT_OUT_RGBA8 if self.rgba8 else 0))
         return p
 
     def rows(self, height: int) -> int:
@@ -285,14 +295,14 @@ class Renderer:
                                 self.scene.height), self._ctx)
 
     def render(self, params: RenderParams | None = None, out=None, stream=None):
-        """Render into host memory (returns (rows, W, 4) float32, or uint16
-        bits for fp16), or into a device tensor ``out`` (anything with
+        """Render into host memory (returns (rows, W, 4) float32, uint16 bits
+        for fp16, uint8 for rgba8), or into a device tensor ``out`` (anything with
         ``data_ptr()``) enqueued on ``stream`` (a raw hipStream_t int / torch
         stream; default torch's current stream) without a host sync."""
         p = params or RenderParams()
         if out is None:
             rows = p.rows(self.scene.height)
-            dt = np.uint16 if p.fp16 else np.float32
+            dt = np.uint8 if p.rgba8 else np.uint16 if p.fp16 else np.float32
             img = np.empty((rows, self.scene.width, 4), dtype=dt)
             _check(lib.rt_render(self._ctx, ctypes.byref(p.c()),
                                  img.ctypes.data_as(ctypes.c_void_p)), self._ctx)
@@ -307,30 +317,34 @@ class Renderer:
                                    ctypes.c_void_p(ptr), ctypes.c_void_p(stream)), self._ctx)
         return out
 
-    def render_progressive(self, params: RenderParams, batch_spp: int, out, stream=None):
+    def render_progressive(self, params: RenderParams, batch_spp: int, out, stream=None,
+                           gather: bool = False):
         """Progressive accumulation: ``params.spp`` samples as
         launches of ``batch_spp`` samples into the context's running fp32 sums
         (``RT_KEEP_SUM`` / ``accumulate`` with ``sample_base`` advancing), all
         enqueued on ``stream``; the last launch writes the averaged frame to the
-        device tensor ``out``.  Bit-identical to one launch of ``params.spp``."""
+        device tensor ``out``.  Bit-identical to one launch of ``params.spp``.
+        ``gather``: every launch goes through rt_render_gather (this rank's rows
+        of the communicator's partition), the last one gathers the frame into
+        ``out`` on rank 0 -- one RCCL gather per frame."""
         if stream is None:
             import torch
             stream = torch.cuda.current_stream().cuda_stream
         elif hasattr(stream, "cuda_stream"):
             stream = stream.cuda_stream
         total, done = params.spp, 0
-        ptr = out if isinstance(out, int) else out.data_ptr()
+        ptr = out if (out is None or isinstance(out, int)) else out.data_ptr()
         while done < total:
             n = min(batch_spp, total - done)
             last = done + n == total
             p = RenderParams(spp=n, bounces=params.bounces, sample_base=params.sample_base + done,
                              row_start=params.row_start, row_step=params.row_step,
                              row_count=params.row_count, accumulate=done > 0, keep_sum=True,
-                             fp16=params.fp16)
+                             fp16=params.fp16, rgba8=params.rgba8)
             flags = RT_OUT_DEVICE if last else (RT_OUT_DEVICE | RT_OUT_NONE)
-            _check(lib.rt_render_async(self._ctx, ctypes.byref(p.c(flags)),
-                                       ctypes.c_void_p(ptr if last else None),
-                                       ctypes.c_void_p(stream)), self._ctx)
+            fn = lib.rt_render_gather if gather else lib.rt_render_async
+            _check(fn(self._ctx, ctypes.byref(p.c(flags)), ctypes.c_void_p(ptr if last else None),
+                      ctypes.c_void_p(stream)), self._ctx)
             done += n
         return out
 
@@ -361,6 +375,47 @@ class Renderer:
         _check(lib.rt_render_mis(self._ctx, ctypes.byref(p.c(RT_OUT_DEVICE)), ptr(out), ptr(out8)),
                self._ctx)
         return out, out8
+
+    def comm_init(self, rank: int, world: int, comm_id: bytes):
+        """rt_comm_init: join the world-rank RCCL communicator (collective)."""
+        if len(comm_id) != RT_COMM_ID_BYTES:
+            raise ValueError("comm_id must be the 128 bytes of rt_comm_unique_id()")
+        buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES).from_buffer_copy(comm_id)
+        _check(lib.rt_comm_init(self._ctx, rank, world, buf), self._ctx)
+        self.rank, self.world = rank, world
+
+    def render_gather(self, params: RenderParams | None = None, out=None, stream=None):
+        """rt_render_gather (collective): this rank renders rows y = rank (mod
+        world), the tiles are gathered over RCCL into the frame on rank 0.
+        Host: returns the (H, W, 4) frame on rank 0 (None elsewhere).  Device:
+        ``out`` (rank 0; anything with ``data_ptr()``) is filled on ``stream``
+        without a host sync."""
+        p = params or RenderParams()
+        if out is None:
+            frame = None
+            if getattr(self, "rank", 0) == 0 and not (p.c().flags & RT_OUT_NONE):
+                dt = np.uint8 if p.rgba8 else np.uint16 if p.fp16 else np.float32
+                frame = np.empty((self.scene.height, self.scene.width, 4), dtype=dt)
+            ptr = None if frame is None else frame.ctypes.data_as(ctypes.c_void_p)
+            _check(lib.rt_render_gather(self._ctx, ctypes.byref(p.c()), ptr, None), self._ctx)
+            return frame
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream().cuda_stream
+        elif hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        ptr = out if isinstance(out, int) else out.data_ptr()
+        _check(lib.rt_render_gather(self._ctx, ctypes.byref(p.c(RT_OUT_DEVICE)), ctypes.c_void_p(ptr),
+                                    ctypes.c_void_p(stream)), self._ctx)
+        return out
+
+    def last_launch(self) -> dict:
+        """The kernel instantiation and launch shape of the last render
+        (rt_last_launch): kernel name as rocprofv3 reports it, lanes per
+        pixel, whether the LDS Halton tables were filled, grid, LDS bytes."""
+        info = LaunchInfo()
+        _check(lib.rt_last_launch(self._ctx, ctypes.byref(info)), self._ctx)
+        return info.as_dict()
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()

@@ -20,3 +20,7 @@ def kernel_source_sha() -> str:
                 h.update(f.encode())
                 h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
+
+
+if __name__ == "__main__":  # the Makefile compiles this into librtpt.so (rt_build_sha)
+    print(kernel_source_sha())

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RTPT_ABI_VERSION 3
+#define RTPT_ABI_VERSION 4
 
 /* Maximum bounce count: Halton dimensions 2+5b..5+5b must stay inside the
  * 24-entry `primes[]` table (`RTrace/sampling.metal:97-104`); b <= 3. */
@@ -71,6 +71,12 @@ typedef struct rt_scene_desc {
 #define RT_KEEP_SUM   0x8u  /* also write the running per-pixel sum into the context,
                                so that a following call may set accumulate=1
                                (progressive rendering)               */
+#define RT_OUT_RGBA8  0x10u /* store the reference's 8-bit image instead (4 B/px):
+                               the epilogue of RTrace/image.swift:35-65 fused into
+                               the kernel's store -- rgba16F round trip
+                               (renderer.swift:74-82), x2 exposure, Reinhard,
+                               pow(v, 1/2.2), clamp, truncating UInt8, alpha 255.
+                               Exclusive with RT_OUT_FP16.                         */
 
 typedef struct rt_render_params {
     uint32_t spp;          /* samples this call (reference: 400, raytrace.metal:24) */
@@ -80,9 +86,11 @@ typedef struct rt_render_params {
     uint32_t row_step;     /*   j = 0..row_count-1 (multi-GPU interleaved tiles)    */
     uint32_t row_count;    /*   0 => all rows                                      */
     uint32_t accumulate;   /* 1: continue the context's running per-pixel sum,
-                              which must then hold exactly samples
-                              [0, sample_base) of the same rows (written by a
-                              previous call with RT_KEEP_SUM)                       */
+                              which must then hold the samples [first,
+                              sample_base) of the same rows, written by previous
+                              calls with RT_KEEP_SUM (the first of them started
+                              at sample index `first`); the image is the sum
+                              divided by the samples it holds                      */
     uint32_t flags;        /* RT_OUT_* */
 } rt_render_params;
 
@@ -101,8 +109,8 @@ int rt_set_seeds(rt_ctx* ctx, const uint32_t* seeds, int32_t width, int32_t heig
 int rt_fill_seeds(rt_ctx* ctx, uint64_t key);
 
 /* Renderer.draw(): render and block until done (commit+waitUntilCompleted).
- * out: row_count*W pixels, rgba32F (16 B) or rgba16F (8 B) by flags; value
- * (sum/S, 1) where S = samples in the sum. */
+ * out: row_count*W pixels, rgba32F (16 B), rgba16F (8 B) or RGBA8 (4 B) by
+ * flags; value (sum/S, 1) where S = samples in the sum. */
 int rt_render(rt_ctx* ctx, const rt_render_params* params, void* out);
 
 /* Asynchronous variant: enqueue on `hip_stream` (a hipStream_t, may be NULL
@@ -115,6 +123,56 @@ int rt_render_async(rt_ctx* ctx, const rt_render_params* params, void* out_devic
 int rt_last_kernel_ms(rt_ctx* ctx, float* ms);
 
 int rt_destroy(rt_ctx* ctx);
+
+/* ---- multi-GPU: row-interleaved tiles + one RCCL gather ----
+ * north_star: "the image is row-tile-partitioned across the 8 GPUs of one node
+ * with a single RCCL gather of tiles over xGMI at the end of each spp batch".
+ * One process (or thread) per GPU, one context per GPU.  Rank k of N renders
+ * the rows y = k, k+N, k+2N, ... with the global y (so the frame is
+ * bit-identical to a single-GPU render) and the tiles are gathered to rank 0
+ * by one ncclGather over xGMI, then placed at their rows by one strided copy
+ * per rank.  The reference's draw (renderer.swift:117-146) has no multi-GPU
+ * path; this extends it. */
+#define RT_COMM_ID_BYTES 128   /* ncclUniqueId */
+
+/* Rank 0 makes the communicator id and hands it to every rank out of band
+ * (MPI, a TCP store, a file).  RT_ERR_COMM on failure. */
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+
+/* Join the N-rank communicator (collective: every rank calls it with the same
+ * id).  RT_ERR_INVALID_ARG for a bad rank/world, RT_ERR_COMM for RCCL errors,
+ * RT_ERR_STATE if the context already has a communicator. */
+int rt_comm_init(rt_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RT_COMM_ID_BYTES]);
+
+/* Renderer.draw() across the communicator (collective): render this rank's
+ * rows with params (which name the whole frame: row_start 0, row_step 0 or 1,
+ * row_count 0; the partition is y = rank (mod world)), then gather every tile into `frame` on rank 0 --
+ * H*W pixels in the format of params->flags (rgba32F / rgba16F / RGBA8), host
+ * memory (the call then blocks) or device memory with RT_OUT_DEVICE (enqueued
+ * on `hip_stream`, NULL = the context's stream, no host sync).  `frame` is
+ * ignored on other ranks.  With RT_OUT_NONE (progressive batches into the
+ * running sums) nothing is gathered.  RT_ERR_STATE without rt_comm_init,
+ * RT_ERR_COMM when the gather fails. */
+int rt_render_gather(rt_ctx* ctx, const rt_render_params* params, void* frame, void* hip_stream);
+
+/* Which kernel instantiation the most recent rt_render/rt_render_async
+ * launched, with its launch shape: lets a caller (bench, tests) state which
+ * configuration it timed or checked.  `kernel` is the demangled name rocprofv3
+ * reports, e.g. "rt::path_trace_kernel<3, 6, false, true, 4>". */
+typedef struct rt_launch_info {
+    char kernel[96];
+    uint32_t lanes_per_pixel;   /* 1, 4 or 16 lanes trace one pixel's samples     */
+    uint32_t halton_tables;     /* 1: LDS low-digit Halton tables filled (§3.3)   */
+    uint32_t small_index;       /* 1: fixed-digit Halton (max index < 3^13)       */
+    uint32_t block_threads;
+    uint32_t grid_x, grid_y;
+    uint32_t lds_bytes;         /* dynamic LDS per workgroup                      */
+} rt_launch_info;
+int rt_last_launch(const rt_ctx* ctx, rt_launch_info* info);
+
+/* Hash of the sources this library was built from (gpuraytracer_amd/srchash.py:
+ * csrc/ + include/): a loader can refuse a stale binary. */
+const char* rt_build_sha(void);
 
 /* Diagnostic counters of a -DRT_STATS build of the kernel (reads and clears
  * up to 16 uint64 counters; RT_ERR_STATE in normal builds). */

@@ -712,6 +712,13 @@ static float f16_to_f32(uint16_t h) {
     return f;
 }
 
+/* RTrace/image.swift:35-65: the rgba16F texture read back as Float16
+ * (:35-38; renderer.swift:74-82 is the texture format), then per RGB channel
+ * value *= exposure (2, :41,54); value = value/(value+1) (:55);
+ * value = pow(value, 1/gamma) (gamma 2.2, :42,56); max(0, min(1, value)) (:59);
+ * UInt8(value*255), truncating (:60); alpha 255 (:63).  pow is the contract's
+ * portable pow (pto_pow); a NaN (fp16 inf after Reinhard)
+ * skips it, and min(1.0, NaN) is 1.0 in Swift as in C's fminf. */
 void pto_tonemap_rgba8(const float* in, size_t n, uint8_t* out) {
     const float exposure = 2.0f, gamma = 2.2f;
     for (size_t i = 0; i < n; ++i) {
@@ -719,7 +726,7 @@ void pto_tonemap_rgba8(const float* in, size_t n, uint8_t* out) {
             float v = f16_to_f32(f32_to_f16(in[4 * i + c]));
             v *= exposure;
             v = v / (v + 1.0f);
-            v = powf(v, 1.0f / gamma);
+            if (v == v) v = pto_pow(v, 1.0f / gamma);
             v = fmaxf(0.0f, fminf(1.0f, v));
             out[4 * i + c] = (uint8_t)(v * 255.0f);
         }

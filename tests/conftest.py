@@ -21,11 +21,29 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) — run with -m gpu")
 
 
+def _lib_is_fresh(path):
+    """Whether the built librtpt.so carries this tree's source hash (its
+    rt_build_sha() string), read from the file's bytes: loading it here would
+    map a HIP runtime before the tests choose one."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_rt_srchash", os.path.join(ROOT, "gpuraytracer_amd", "srchash.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # not via the package: that would load the library
+    kernel_source_sha = mod.kernel_source_sha
+    with open(path, "rb") as f:
+        return b"\0" + kernel_source_sha().encode() + b"\0" in f.read()
+
+
 def _ensure_built():
-    need = [os.path.join(ROOT, "gpuraytracer_amd", "librtpt.so"),
-            os.path.join(ROOT, "oracle", "liboracle.so")]
-    if not all(os.path.exists(p) for p in need):
+    lib = os.path.join(ROOT, "gpuraytracer_amd", "librtpt.so")
+    need = [lib, os.path.join(ROOT, "oracle", "liboracle.so")]
+    fresh = all(os.path.exists(p) for p in need) and _lib_is_fresh(lib)
+    if not fresh:  # missing, or built from other sources than this tree
         subprocess.check_call(["make", "-C", ROOT, "-j8"], stdout=subprocess.DEVNULL)
+    orc = os.path.join(ROOT, "oracle")
+    if os.path.getmtime(os.path.join(orc, "pt_oracle.c")) > os.path.getmtime(need[1]):
+        subprocess.check_call(["make", "-C", orc], stdout=subprocess.DEVNULL)
 
 
 _ensure_built()

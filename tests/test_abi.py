@@ -99,3 +99,80 @@ def test_scene_layout_uses_shared_edge_pairs():
     assert info["sphere_bvh_lds_bytes"] == 6 * 112 + 2 * 1999 * 16 + 2 * 1999 * 2
     big = g.Scene.random_spheres(16, 8, 5000).describe()
     assert big["lds_bytes"] == 6 * 112 and big["sphere_bvh_lds_bytes"] == 0 and big["n_sphere_nodes"] == bvh_nodes(5000)
+
+
+def test_library_carries_the_tree_source_hash():
+    """librtpt.so was built from exactly these sources (rt_build_sha, compiled
+    in by the Makefile from gpuraytracer_amd/srchash.py); the loader refuses a
+    mismatching binary."""
+    from gpuraytracer_amd.srchash import kernel_source_sha
+    assert g.lib.rt_build_sha().decode() == kernel_source_sha()
+
+
+def test_last_launch_needs_a_render():
+    info = _native.LaunchInfo()
+    assert g.lib.rt_last_launch(None, ctypes.byref(info)) == 1
+
+
+def _tonemap_inputs():
+    rng = np.random.default_rng(3)
+    v = np.concatenate([
+        np.array([0.0, 1e-30, 6e-8, 1e-4, 0.05, 0.5, 1.0, 3.0, 65504.0, 65520.0, 1e6, np.inf],
+                 np.float32),
+        rng.exponential(0.3, 20000).astype(np.float32),
+        rng.uniform(0, 50, 5000).astype(np.float32)])
+    a = np.zeros((len(v), 4), np.float32)
+    a[:, 0], a[:, 1], a[:, 2], a[:, 3] = v, v[::-1], np.roll(v, 7), 1.0
+    return a
+
+
+def test_host_tonemap_equals_oracle_tonemap():
+    """rt_tonemap_rgba8 (host form of the kernel's RT_OUT_RGBA8 epilogue,
+    rt::tonemap_channel) == the oracle's image.swift:35-65 restatement, incl.
+    fp16 overflow (inf -> NaN after Reinhard -> 255, Swift min(1, NaN) = 1)."""
+    import oracle_lib
+    a = _tonemap_inputs()
+    ours = g.tonemap_rgba8(a)
+    assert np.array_equal(ours, oracle_lib.tonemap(a))
+    assert ours[9, 0] == 255 and ours[11, 0] == 255  # 65520 and inf overflow fp16
+    assert np.all(ours[:, 3] == 255)
+
+
+def test_tonemap_contract_pow_vs_libm():
+    """The contract's portable pow against float32 libm pow
+    in a numpy restatement of image.swift:41-60: a byte can differ only where
+    v*255 sits within the pow error of an integer."""
+    a = _tonemap_inputs()[:, :3]
+    v = a.astype(np.float16).astype(np.float32) * np.float32(2.0)
+    with np.errstate(invalid="ignore"):
+        v = v / (v + np.float32(1.0))
+        p = np.power(v, np.float32(1.0) / np.float32(2.2))
+    p = np.where(np.isnan(p), np.float32(1.0), np.clip(p, 0, 1))
+    ref = (p * np.float32(255.0)).astype(np.uint8)
+    ours = g.tonemap_rgba8(_tonemap_inputs())[:, :3]
+    diff = ours.astype(int) - ref.astype(int)
+    assert np.abs(diff).max() <= 1
+    near = np.abs(p * 255.0 - np.round(p * 255.0)) < 1e-3
+    assert np.all(near[diff != 0])
+
+
+def test_comm_entry_points_reject_bad_arguments():
+    """rt_comm_init / rt_render_gather / rt_comm_unique_id argument errors come
+    back as status codes without a device (the RCCL calls are never reached)."""
+    buf = (ctypes.c_uint8 * _native.RT_COMM_ID_BYTES)()
+    assert g.lib.rt_comm_unique_id(None) == 1
+    assert g.lib.rt_comm_init(None, 0, 1, buf) == 1
+    assert g.lib.rt_render_gather(None, None, None, None) == 1
+    assert b"null" in g.lib.rt_last_error(None)
+
+
+def test_bench_multi_gpu_launcher_needs_the_gpus():
+    """`bench.py --gpus N` outside torchrun spawns its own N ranks; with fewer
+    visible GPUs it stops before spawning, with a clear message."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES=""))
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr
