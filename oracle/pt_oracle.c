@@ -240,6 +240,24 @@ static int closest(const scene_t* s, v3 o, v3 d, float tmin, float tmax, float* 
     return id;
 }
 
+/* Primitive id of the closest hit of each pixel's camera ray through the
+ * pixel centre (jitter 0.5, 0.5; sampling.metal:125-157 + raytrace.metal:48-49),
+ * -1 on a miss: the scene geometry as the camera sees it, compared with the
+ * reference's example.png (tests/test_oracle.py). ids: H*W int32. */
+int pto_primary_ids(const CameraGPU* cam, const MaterialGPU* mats, const SquareLightGPU* light,
+                    const rt_float3* verts, uint32_t n_tri, int32_t* ids) {
+    scene_t s;
+    if (scene_build(&s, cam, mats, light, verts, n_tri, NULL, 0) != 0) return -1;
+    for (int32_t y = 0; y < s.cam.H; ++y)
+        for (int32_t x = 0; x < s.cam.W; ++x) {
+            float t;
+            ids[(size_t)y * s.cam.W + x] =
+                closest(&s, s.cam.pos, cam_dir(&s.cam, x, y, 0.5f, 0.5f), 0.001f, 1000.0f, &t);
+        }
+    scene_free(&s);
+    return 0;
+}
+
 /* any hit, accept_any_intersection(true) (raytrace.metal:79-85) */
 static int occluded(const scene_t* s, v3 o, v3 d, float tmin, float tmax) {
     float t;

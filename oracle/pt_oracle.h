@@ -91,6 +91,11 @@ float pto_pow(float x, float y);
 /* image.swift:35-65 epilogue */
 void pto_tonemap_rgba8(const float* rgba32f, size_t n_pixels, uint8_t* rgba8);
 
+/* Closest-hit primitive id of every pixel's camera ray through the pixel
+ * centre (-1: miss), H*W int32 (geometry check against example.png). */
+int pto_primary_ids(const CameraGPU* cam, const MaterialGPU* mats, const SquareLightGPU* light,
+                    const rt_float3* verts, uint32_t n_tri, int32_t* ids);
+
 /* Count of ray/primitive tests issued by one render (for the VALU roofline). */
 uint64_t pto_last_tests(void);
 

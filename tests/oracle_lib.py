@@ -47,6 +47,19 @@ def render(scene, seeds, spp, bounces=3, sample_base=0, row_start=0, row_step=1,
     return (out, s_out) if want_sum else out
 
 
+_lib.pto_primary_ids.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_void_p]
+
+
+def primary_ids(scene):
+    """Closest-hit primitive id of every pixel's camera ray through the pixel
+    centre (-1: miss), (H, W) int32 -- pto_primary_ids."""
+    ids = np.empty((scene.height, scene.width), np.int32)
+    r = _lib.pto_primary_ids(_p(scene.camera), _p(scene.materials), _p(scene.light),
+                             _p(scene.vertices), scene.n_triangles, _p(ids))
+    assert r == 0
+    return ids
+
+
 def cornell_box(width, height):
     cam, light = CameraGPU(), SquareLightGPU()
     mats, verts, n = (MaterialGPU * 36)(), (float3 * 108)(), ctypes.c_uint32()

@@ -389,3 +389,62 @@ def test_mis_light_pixels_known_answer():
     expect = (M.pow_pt(tm, np.float32(1) / np.float32(2.2)) * np.float32(255)).astype(np.uint8)
     assert np.all(out8[lit][:, :3] == expect) and np.all(out8[..., 3] == 255)
     assert np.all(out[..., 3] == 6)
+
+
+def test_geometry_matches_reference_example_png():
+    """The live scene as the oracle's camera sees it (primary-hit ids through
+    the pixel centres, 800x600 = scene.swift:18) against the geometry measured
+    from the reference's example.png (tests/golden/make_example_masks.py):
+    colour classes (open front = black, red wall, green wall, light) and every
+    luminance step the image shows along 54 rows and 74 columns -- the walls'
+    floor/ceiling lines, both boxes' silhouettes and creases, the light's rim.
+    Pins geometry only: the PNG is an earlier revision, its radiance is not a
+    fixture (parity of radiance stays unpinned)."""
+    g = np.load(os.path.join(GOLDEN, "example_png_geometry.npz"))
+    ids = oracle_lib.primary_ids(Scene.cornell_box(800, 600))
+    ocls = np.full(ids.shape, 4, np.uint8)
+    ocls[ids < 0] = 0
+    ocls[(ids == 2) | (ids == 3)] = 1      # red wall (scene.swift:93-102)
+    ocls[(ids == 4) | (ids == 5)] = 2      # green wall (:105-114)
+    ocls[(ids == 34) | (ids == 35)] = 3    # the light (:58-59)
+    cls = g["cls"]
+    assert (ocls == cls).mean() >= 0.99
+    # IoU bars: the light is a 113 x 22 px patch, whose one-pixel rim alone is
+    # ~11 % of its area (measured 0.953); the large regions agree to >= 0.97
+    for c, name, bar in [(0, "open front", 0.97), (1, "red wall", 0.97),
+                         (2, "green wall", 0.97), (3, "light", 0.95)]:
+        a, b = cls == c, ocls == c
+        iou = (a & b).sum() / (a | b).sum()
+        assert iou >= bar, f"{name}: IoU {iou:.4f}"
+    face = np.where(ids < 0, -1, ids // 2)  # a quad's two triangles form one face
+    floor = 3                               # ids 6-7 (:117-126)
+    unmatched, on_floor, offs = [], 0, []
+    # a step measured on line L at position p was smoothed over lines L-4..L+4
+    # (the 9-px filter across the line): it matches a face boundary along any
+    # of those lines within +-3 px of p
+    for (line, pos), axis in [(e, 0) for e in g["row_edges"]] + [(e, 1) for e in g["col_edges"]]:
+        best = None
+        for ln in range(max(0, line - 4), min(face.shape[axis] if axis else face.shape[0], line + 5)):
+            prof = face[ln] if axis == 0 else face[:, ln]
+            near = [abs(k - pos) for k in range(max(1, pos - 3), min(len(prof), pos + 4))
+                    if prof[k] != prof[k - 1]]
+            if near and (best is None or min(near) < best):
+                best = min(near)
+        if best is not None:
+            offs.append(best)
+        else:
+            unmatched.append((axis, int(line), int(pos)))
+            on_floor += int((face[line, pos] if axis == 0 else face[pos, line]) == floor)
+    n = len(g["row_edges"]) + len(g["col_edges"])
+    # every step the image shows is a face boundary of the live scene within
+    # +-3 px, except the floor's shadow edges (lighting, not geometry)
+    assert on_floor == len(unmatched), [u for u in unmatched]
+    assert len(unmatched) <= 0.1 * n, len(unmatched)
+    assert np.median(offs) <= 1 and len(offs) >= 0.9 * n
+    # both boxes' silhouettes are among the matched steps (scene.swift:141-172)
+    for lo, hi in [(10, 22), (22, 34)]:
+        box = (ids >= lo) & (ids < hi)
+        ys, xs = np.nonzero(box)
+        edges_on_box = [(y, x) for y, x in g["row_edges"]
+                        if box[y].any() and min(abs(x - xs[ys == y].min()), abs(x - 1 - xs[ys == y].max())) <= 3]
+        assert edges_on_box, f"no image edge on the silhouette of box ids {lo}-{hi - 1}"
