@@ -83,26 +83,13 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     lc = lc * saturate(dot(-L, f3{0.0f, -1.0f, 0.0f}));
     lc = lc * saturate(dot(N, L));                         // :75
     s.thr = s.thr * diffuse;                               // :76
+    // the light term lc * throughput (:87-89) and the next direction (:93-100)
+    // are formed BEFORE the shadow query: the same operations, but the shading
+    // frame N/right/fwd and lc are dead during the walk (6-9 fewer live VGPRs)
+    const f3 contrib = lc * s.thr;
     const f3 seg_lo{fminf(p.x, q.x), fminf(p.y, q.y), fminf(p.z, q.z)};
     const f3 seg_hi{fmaxf(p.x, q.x), fmaxf(p.y, q.y), fmaxf(p.z, q.z)};
-    if (FUSE && b + 1 < B) {
-        const float cu = halton_dim<4 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);           // :93-94
-        const float cv = halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
-        float sp, cp;
-        sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
-        const float ct = sqrtf(cv);
-        const float st = sqrtf(1.0f - ct * ct);
-        const f3 d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
-        const FusedHit h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
-        if (!h.occluded) s.acc = s.acc + lc * s.thr;       // :79-89
-        s.d = d2;
-        s.o = p;                                           // :99-100
-        *nid = h.id;
-        *nt = h.t;
-        return true;
-    }
-    if (!any_hit<GEO, SPH, (b == 0 && RT_SPH_PACKET) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
-        s.acc = s.acc + lc * s.thr;                        // :87-89
+    f3 d2{0.0f, 0.0f, 0.0f};
     if (b + 1 < B) {                                       // last direction never traced
         const float cu = halton_dim<4 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);           // :93-94
         const float cv = halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
@@ -110,7 +97,21 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
         const float ct = sqrtf(cv);
         const float st = sqrtf(1.0f - ct * ct);
-        s.d = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
+        d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
+    }
+    if (FUSE && b + 1 < B) {
+        const FusedHit h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
+        if (!h.occluded) s.acc = s.acc + contrib;          // :79-89
+        s.d = d2;
+        s.o = p;                                           // :99-100
+        *nid = h.id;
+        *nt = h.t;
+        return true;
+    }
+    if (!any_hit<GEO, SPH, (b == 0 && RT_SPH_PACKET) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
+        s.acc = s.acc + contrib;                           // :87-89
+    if (b + 1 < B) {
+        s.d = d2;
         s.o = p;                                           // :99-100
     }
     return true;
@@ -404,40 +405,62 @@ void path_trace_kernel(KParams P) {
     // wave = 64/L pixels: 8x8 (L=1), 4x4 (L=4), 2x2 (L=16), or one row of 64/L
     // pixels for interleaved rows (launcher's wave_w); workgroup = 2x2 waves
     const uint32_t kWX = (L == 1) ? 8u : P.wave_w, kWY = (64u / L) / kWX;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t pix = lane / L, sub = lane % L;
-    const uint32_t x = blockIdx.x * (WR * kWX) + (wave % WR) * kWX + (pix % kWX);
-    const uint32_t j = blockIdx.y * (WR * kWY) + (wave / WR) * kWY + (pix / kWX);
-    if (x >= (uint32_t)P.W || j >= P.row_count) return;  // a pixel's L lanes leave together
-    const uint32_t y = P.row_start + j * P.row_step;
-    const size_t o = (size_t)j * (size_t)P.W + x;
-
-    const uint32_t seed = P.seeds[(size_t)y * (size_t)P.W + x];  // raytrace.metal:37
-    f3 lum{0.0f, 0.0f, 0.0f};                                    // :32
-    if (P.accumulate) {
-        const float4 prev = P.sum[o];
-        lum = f3{prev.x, prev.y, prev.z};
+    auto pixel_of = [&](uint32_t t, uint32_t& x, uint32_t& j) {
+        const uint32_t lane = t & 63u, wave = t >> 6, pix = lane / L;
+        x = blockIdx.x * (WR * kWX) + (wave % WR) * kWX + (pix % kWX);
+        j = blockIdx.y * (WR * kWY) + (wave / WR) * kWY + (pix / kWX);
+    };
+    // Per-lane constants (pixel coordinates, lane roles) are recomputed from an
+    // opaque copy of threadIdx.x where they are used, and the seed is kept in
+    // LDS: otherwise the compiler hoists them out of the sample loop and spills
+    // them to scratch for the whole launch (36 B/lane of scratch writes).
+    auto opaque_tid = []() {
+        uint32_t t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+    {
+        uint32_t x, j;
+        pixel_of(threadIdx.x, x, j);
+        if (x >= (uint32_t)P.W || j >= P.row_count) return;  // a pixel's L lanes leave together
     }
-    // L > 1: the pixel's running sum lives in LDS (its group leader adds to it),
-    // which keeps three VGPRs free across the path traversal
+    __shared__ uint32_t seed_s[NT];        // seed + sample_base of the lane's pixel
     __shared__ float lum_s[L > 1 ? 3 * (NT / L) : 1];
-    const uint32_t slot = threadIdx.x / L;
-    if (L > 1 && sub == 0) {
-        lum_s[3 * slot] = lum.x;
-        lum_s[3 * slot + 1] = lum.y;
-        lum_s[3 * slot + 2] = lum.z;
+    f3 lum{0.0f, 0.0f, 0.0f};                                    // :32
+    {
+        const uint32_t t = threadIdx.x, sub = t % L;
+        uint32_t x, j;
+        pixel_of(t, x, j);
+        const uint32_t y = P.row_start + j * P.row_step;
+        seed_s[t] = P.seeds[(size_t)y * (size_t)P.W + x] + P.sample_base;  // raytrace.metal:37
+        if (P.accumulate) {
+            const float4 prev = P.sum[(size_t)j * (size_t)P.W + x];
+            lum = f3{prev.x, prev.y, prev.z};
+        }
+        // L > 1: the pixel's running sum lives in LDS (its group leader adds to
+        // it), which keeps three VGPRs free across the path traversal
+        const uint32_t slot = t / L;
+        if (L > 1 && sub == 0) {
+            lum_s[3 * slot] = lum.x;
+            lum_s[3 * slot + 1] = lum.y;
+            lum_s[3 * slot + 2] = lum.z;
+        }
     }
     const f3 cu = ld_f3(P.cam_u), cv = ld_f3(P.cam_v), cw = ld_f3(P.cam_w);
-    const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
+    const float fW = (float)P.W, fH = (float)P.H;
     const uint32_t rounds = (P.spp + (L - 1)) / L;
     for (uint32_t r = 0; r < rounds; ++r) {                      // :34
+        const uint32_t t = opaque_tid(), sub = t % L;
         // a lane past the last sample re-traces the last one (discarded below):
         // no divergent branch around the path
         const uint32_t n = (L == 1) ? r : min(r * L + sub, P.spp - 1u);
         PathState s;
         s.acc = f3{0.0f, 0.0f, 0.0f};
         {
-            s.i = seed + (P.sample_base + n);
+            uint32_t x, j;
+            pixel_of(t, x, j);
+            const float fx = (float)x, fy = (float)(P.row_start + j * P.row_step);
+            s.i = seed_s[t] + n;                                 // seed + (sample_base + n)
             const float jx = halton_dim<0, SMALL>(s.i);                                // :39-40
             const float jy = halton_dim<1, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
             // generateCameraRay (sampling.metal:125-157)
@@ -452,13 +475,14 @@ void path_trace_kernel(KParams P) {
         if (L == 1) {
             lum = lum + s.acc;                                   // :103
         } else {
-            const int base = (int)(lane - sub);
+            const uint32_t t2 = opaque_tid(), lane = t2 & 63u, sub2 = t2 % L, slot = t2 / L;
+            const int base = (int)(lane - sub2);
             f3 c[L];
 #pragma unroll
             for (int k = 0; k < L; ++k)                          // samples r*L + k
                 c[k] = f3{__shfl(s.acc.x, base + k), __shfl(s.acc.y, base + k),
                           __shfl(s.acc.z, base + k)};
-            if (sub == 0) {
+            if (sub2 == 0) {
                 f3 acc{lum_s[3 * slot], lum_s[3 * slot + 1], lum_s[3 * slot + 2]};
 #pragma unroll
                 for (int k = 0; k < L; ++k)                      // in sample order
@@ -469,10 +493,15 @@ void path_trace_kernel(KParams P) {
             }
         }
     }
+    const uint32_t t = opaque_tid();
     if (L > 1) {
-        if (sub != 0) return;
+        if (t % L != 0) return;
+        const uint32_t slot = t / L;
         lum = f3{lum_s[3 * slot], lum_s[3 * slot + 1], lum_s[3 * slot + 2]};
     }
+    uint32_t x, j;
+    pixel_of(t, x, j);
+    const size_t o = (size_t)j * (size_t)P.W + x;
     if (P.sum) P.sum[o] = make_float4(lum.x, lum.y, lum.z, (float)P.samples_total);
     if (P.out) {
         const float fs = (float)P.samples_total;                 // :106
@@ -730,6 +759,11 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     if (geo == kGeoPairLds && mem == SceneMem::kPairSorted &&
         lds_bytes + sorted_lds_extra_bytes() <= kMaxLdsBytes)
         geo = kGeoPairSorted;
+#ifdef RT_DEV_ISA  // ISA-inspection builds only (tools/isa.sh): the two headline layouts at B = 3
+    if (bounces != 3) return hipErrorInvalidValue;
+    return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_total, stream)
+                              : launch_g<3, kGeoSphLds>(P, lds_total, stream);
+#endif
     switch (bounces) {
         case 0: return launch_b<0>(P, geo, lds_total, stream);
         case 1: return launch_b<1>(P, geo, lds_total, stream);

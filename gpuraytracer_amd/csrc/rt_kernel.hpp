@@ -17,7 +17,8 @@ constexpr uint32_t kOutRgba8 = 0x10u;  // fused image.swift:35-65 epilogue, ucha
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
 // dynamic LDS of the sphere-BVH-in-LDS kernel: two 1024-thread workgroups per
 // CU share 160 KB with their static per-pixel sums (3 KB at 4 lanes per pixel)
-constexpr size_t kSphLdsMaxBytes = 76 * 1024;
+// and per-lane seeds (4 KB): 80 KB - 7 KB each
+constexpr size_t kSphLdsMaxBytes = 73 * 1024;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
