@@ -785,10 +785,10 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
 
 hipError_t read_debug_stats(unsigned long long* out, int n) {
 #ifdef RT_STATS
-    if (n > 16) n = 16;
+    if (n > 32) n = 32;
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stats), n * sizeof(unsigned long long));
     if (e != hipSuccess) return e;
-    const unsigned long long zero[16] = {0};
+    const unsigned long long zero[32] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_rt_stats), zero, sizeof(zero));
 #else
     (void)out;

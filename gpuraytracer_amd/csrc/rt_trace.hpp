@@ -102,9 +102,8 @@ __device__ __forceinline__ bool sph_test(const float4& S, f3 o, f3 d, float a, f
     if (disc > 0.0f) {
         const float sq = sqrtf(disc);
         const float a2 = 2.0f * a;
-        const float t1 = (-b - sq) / a2;
-        const float t2 = (-b + sq) / a2;
-        const float t = (t1 > tmin) ? t1 : t2;
+        float t = (-b - sq) / a2;                 // t1
+        if (!(t > tmin)) t = (-b + sq) / a2;      // t2, divided only when it is the root taken
         if (t > tmin && t < tmax) {
             *t_out = t;
             return true;
@@ -119,8 +118,12 @@ __device__ __forceinline__ bool sph_test(const float4& S, f3 o, f3 d, float a, f
 // tested, [4q+2] active lanes summed over tested records, [4q+3] division blocks.
 // Box-cluster queries: [12] queries per wave, [13] candidate rounds per wave,
 // [14] lanes summed over rounds, [15] lanes summed over queries.
+// Sphere walks (sphere_walk_lds), base 16 closest / 24 any-hit: [+0] walks per
+// wave, [+1] lanes summed over walks, [+2] cheap-step iterations, [+3] lanes
+// summed over them, [+4] unused, [+5] root rounds, [+6] parked lanes summed
+// over them.  [23] packet walks, [31] packet walk iterations.
 #ifdef RT_STATS
-__device__ unsigned long long g_rt_stats[16];
+__device__ unsigned long long g_rt_stats[32];
 __device__ __forceinline__ void stat_wave(int slot, unsigned long long v) {
     const unsigned long long m = __ballot(1);
     if ((threadIdx.x & 63u) == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(&g_rt_stats[slot], v);
@@ -328,7 +331,9 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
     ent += lay * nN;
     ids += lay * nN;
     uint32_t idx = 0;
+    if (PACKET) RT_STAT(23, 1);
     while (idx < nN) {
+        if (PACKET) RT_STAT(31, 1);
         const uint4 e = ent[idx];
         uint32_t next = idx + 1;
         if (e.w & 0x80000000u) {  // inner node (wave-uniform for PACKET)
@@ -347,6 +352,89 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
             }
         }
         idx = PACKET ? wave_uniform(next) : next;
+    }
+}
+
+// Per-lane walk of the compact LDS BVH with POSTPONED ROOTS (DESIGN.md §3.10;
+// after Aila & Laine's postponed leaf processing, stackless form).  Each step
+// of a lane is cheap and of similar cost whatever the entry: a box test for an
+// inner node, the discriminant of sph_test for a leaf.  A leaf whose
+// discriminant is positive (a real hit candidate) parks the lane with (b, disc);
+// the others walk on until at least half of the lanes still walking are
+// parked (or none can move), then the wave runs the expensive part of the
+// sphere test -- the IEEE sqrt and divisions -- for all parked lanes together.
+// In the plain walk (sphere_closest_lds) a mixed wave pays for the box test,
+// the discriminant AND the roots in most steps.  Per lane the entries are
+// visited in the same order and every value is sph_test's, ranked by (t, id):
+// the same result.  ANY: *id becomes >= 0 on the first accepted hit (and that
+// lane stops).
+template <bool ANY>
+__device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t* ids, uint32_t nN,
+                                                uint32_t nT, f3 o, f3 d, float tmin, float& best,
+                                                int& id) {
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const float a = dot(d, d);
+    const float a4 = 4.0f * a;
+    const RayBox rb = ray_box(o, d);
+    const uint32_t lay = lds_layout(d);
+    ent += lay * nN;
+    ids += lay * nN;
+    uint32_t idx = (ANY && id >= 0) ? nN : 0u;  // next entry of this lane's walk (nN: done)
+    uint32_t leaf = kNone;                      // the parked leaf
+    float pb = 0.0f, pdisc = 0.0f;              // its b and discriminant
+    constexpr int ST = ANY ? 24 : 16;
+    RT_STAT(ST, 1);
+    RT_STAT(ST + 1, __popcll(__ballot(1)));
+    for (;;) {
+        for (;;) {  // cheap steps until the lane parks a leaf or leaves the tree
+            const bool adv = idx < nN && leaf == kNone;
+            if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
+            RT_STAT(ST + 2, 1);
+            RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(adv)));
+            if (adv) {
+                const uint4 e = ent[idx];
+                if (e.w & 0x80000000u) {
+                    idx = lds_node_hit(e, rb, tmin, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
+                } else {  // sph_test up to the discriminant (shaders_old.metal:108-136)
+                    const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y),
+                                         __uint_as_float(e.z)};
+                    const float bq = 2.0f * dot(oc, d);
+                    const float cc = dot(oc, oc) - __uint_as_float(e.w);
+                    const float disc = bq * bq - a4 * cc;
+                    if (disc > 0.0f) {
+                        leaf = idx;
+                        pb = bq;
+                        pdisc = disc;
+                    }
+                    idx = idx + 1;  // a leaf's escape is the next entry
+                }
+            }
+            const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
+            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < nN || leaf != kNone));
+            if (2 * parked >= live) break;
+        }
+        if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
+        RT_STAT(ST + 5, 1);
+        RT_STAT(ST + 6, __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone)));
+        if (leaf != kNone) {  // the roots of the parked leaves (sph_test)
+            const float sq = sqrtf(pdisc);
+            const float a2 = 2.0f * a;
+            float t = (-pb - sq) / a2;
+            if (!(t > tmin)) t = (-pb + sq) / a2;
+            if (ANY) {
+                if (t > tmin && t < best) {
+                    id = 0;
+                    idx = nN;
+                }
+            } else if (t > tmin && t < 3.0e38f && t <= best) {
+                const int s = (int)(nT + ids[leaf]);
+                if (t < best || s < id) {
+                    best = t;
+                    id = s;
+                }
+            }
+            leaf = kNone;
+        }
     }
 }
 
@@ -714,8 +802,10 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
             }
         }
     }
-    if (SPH && GEO == kGeoSphLds)
-        sphere_closest_lds<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
+    if (SPH && GEO == kGeoSphLds && ((CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3))
+        sphere_closest_lds<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
+    else if (SPH && GEO == kGeoSphLds)
+        sphere_walk_lds<false>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
     else if (SPH)
         sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
     *t_io = best;
@@ -770,7 +860,13 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
                 return true;
         }
     }
-    if (SPH && GEO == kGeoSphLds) return sphere_any_lds<PACKET>(sv.sent, sv.nN, o, d, tmin, tmax);
+    if (SPH && GEO == kGeoSphLds && PACKET) return sphere_any_lds<true>(sv.sent, sv.nN, o, d, tmin, tmax);
+    if (SPH && GEO == kGeoSphLds) {
+        float tm = tmax;
+        int id = -1;
+        sphere_walk_lds<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id);
+        return id >= 0;
+    }
     if (SPH) return sphere_any<PACKET>(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
     return false;
 }
