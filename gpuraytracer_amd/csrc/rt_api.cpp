@@ -236,6 +236,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.nS = (uint32_t)c->scene.sph_isect.size();
     K.nP = (uint32_t)c->scene.pair_isect.size();
     K.nN = c->scene.sph_layout_nodes;
+    K.nE = c->scene.sph_lds_entries;
     const rt::CamConst& cam = c->scene.cam;
     memcpy(K.cam_pos, cam.pos, sizeof(K.cam_pos));
     memcpy(K.cam_u, cam.u, sizeof(K.cam_u));

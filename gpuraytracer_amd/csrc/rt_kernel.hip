@@ -365,7 +365,7 @@ void path_trace_kernel(KParams P) {
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
         if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) + entry ids after the pairs
-            const uint32_t ne = 2u * P.nN;
+            const uint32_t ne = 2u * P.nE;
             const uint4* es = reinterpret_cast<const uint4*>(P.sph_lds);
             uint4* ed = reinterpret_cast<uint4*>(lds + ng4);
             for (uint32_t k = threadIdx.x; k < ne; k += NT) ed[k] = es[k];
@@ -399,7 +399,8 @@ void path_trace_kernel(KParams P) {
     sv.nTN = P.nTN;
     sv.node = P.sph_nodes;  // sphere BVH: scalar loads from global memory
     sv.sph = P.sph_isect;
-    sv.nN = SPH ? P.nN : 0u;
+    // sphere walks: BVH nodes per layout (global walks) or compact LDS entries
+    sv.nN = SPH ? (GEO == kGeoSphLds ? P.nE : P.nN) : 0u;
     sv.sph_perm = P.sph_perm;
 
     // wave = 64/L pixels: 8x8 (L=1), 4x4 (L=4), 2x2 (L=16), or one row of 64/L
@@ -740,7 +741,7 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     size_t lds_total = lds_bytes;
     // sphere BVH in LDS (1024-thread workgroups, two per CU) when it fits
     if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto) {
-        const size_t b = lds_bytes + 2u * P.nN * 16u + ((2u * P.nN * 2u + 3u) & ~3u);
+        const size_t b = lds_bytes + 2u * P.nE * 16u + ((2u * P.nE * 2u + 3u) & ~3u);
         if (b <= kSphLdsMaxBytes) {
             geo = kGeoSphLds;
             lds_total = b;

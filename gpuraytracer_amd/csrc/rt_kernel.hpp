@@ -33,7 +33,7 @@ struct KParams {
     const float4* sph_nodes;  // 2 float4 per sphere-BVH node (BvhNode)
     const uint32_t* sph_perm; // BVH leaf order -> sphere id
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
-    const uint32_t* sph_lds;  // compact sphere BVH (2 layouts x nN x 16 B) for LDS, or null
+    const uint32_t* sph_lds;  // compact sphere BVH (2 layouts x nE x 16 B) for LDS, or null
     const uint16_t* sph_lds_id;  // sphere id per compact entry
     const float4* tri_nodes;  // triangle BVH (rt_lbvh.hip): 8 layouts x nTN nodes, or null
     const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
@@ -42,6 +42,7 @@ struct KParams {
     float4* sum;              // running sums (tile layout) or null
     void* out;                // rgba32F / rgba16F tile or null
     uint32_t nT, nP, nS, nN;  // triangles, triangle pairs (0: no pair layout), spheres, BVH nodes
+    uint32_t nE;              // entries per layout of the compact LDS sphere BVH
     uint32_t nTN;             // triangle-BVH nodes per layout (0: no triangle BVH)
     float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
     float halfW, halfH;

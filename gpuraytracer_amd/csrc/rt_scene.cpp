@@ -414,15 +414,38 @@ static uint16_t half_dir(float x, int dir) {
 static void build_sphere_lds(CompiledScene* out) {
     out->sph_lds.clear();
     out->sph_lds_id.clear();
+    out->sph_lds_entries = 0;
     const uint32_t nn = out->sph_layout_nodes;
-    if (nn == 0 || nn > 0x7FFFu || out->sph_isect.size() > 0xFFFFu) return;
+    if (nn == 0 || out->sph_isect.size() > 0xFFFFu) return;
+    // A leaf of c spheres becomes c consecutive sphere entries (each one's
+    // escape is the next entry): the parent's box already bounds them.  Entry
+    // index of every node = prefix sum of the entries of the nodes before it.
+    std::vector<uint32_t> pos(nn + 1);
+    {
+        const BvhNode* L = out->sph_nodes.data();
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < nn; ++i) {
+            pos[i] = k;
+            k += L[i].leaf == 0 ? 1u : (L[i].leaf >> 24);
+        }
+        pos[nn] = k;
+    }
+    const uint32_t ne = pos[nn];  // the same in every layout (a permutation of the same nodes)
+    if (ne > 0x7FFFu) return;
+    out->sph_lds_entries = ne;
     std::vector<uint32_t> ent;
     std::vector<uint16_t> ids;
     for (int oct : {0, 7}) {
         const BvhNode* L = out->sph_nodes.data() + (size_t)oct * nn;
-        for (uint32_t k = 0; k < nn; ++k) {
-            const BvhNode& n = L[k];
-            uint32_t w[4];
+        uint32_t k = 0;  // running entry index of this layout
+        std::vector<uint32_t> lpos(nn + 1);
+        for (uint32_t i = 0; i < nn; ++i) {
+            lpos[i] = k;
+            k += L[i].leaf == 0 ? 1u : (L[i].leaf >> 24);
+        }
+        lpos[nn] = k;
+        for (uint32_t i = 0; i < nn; ++i) {
+            const BvhNode& n = L[i];
             if (n.leaf == 0) {
                 uint16_t h[6];
                 for (int a = 0; a < 3; ++a) {
@@ -430,20 +453,24 @@ static void build_sphere_lds(CompiledScene* out) {
                     h[a] = half_dir(n.lo[a], -1);
                     h[3 + a] = half_dir(n.hi[a], +1);
                 }
-                w[0] = h[0] | (uint32_t)h[1] << 16;
-                w[1] = h[2] | (uint32_t)h[3] << 16;
-                w[2] = h[4] | (uint32_t)h[5] << 16;
-                w[3] = n.escape | 0x80000000u;
+                if (n.escape > nn) return;
+                const uint32_t w[4] = {h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,
+                                       h[4] | (uint32_t)h[5] << 16, lpos[n.escape] | 0x80000000u};
+                ent.insert(ent.end(), w, w + 4);
                 ids.push_back(0);
             } else {
-                if ((n.leaf >> 24) != 1u || n.escape != k + 1) return;  // one sphere per leaf
-                const uint32_t first = n.leaf & 0xFFFFFFu;
-                memcpy(w, out->sph_isect[first].q, 16);
-                if (w[3] & 0x80000000u) return;  // r*r is never negative
-                ids.push_back((uint16_t)out->sph_perm[first]);
+                if (n.escape != i + 1) return;  // a leaf's escape is the next node
+                const uint32_t first = n.leaf & 0xFFFFFFu, cnt = n.leaf >> 24;
+                for (uint32_t j = first; j < first + cnt; ++j) {
+                    uint32_t w[4];
+                    memcpy(w, out->sph_isect[j].q, 16);
+                    if (w[3] & 0x80000000u) return;  // r*r is never negative
+                    ent.insert(ent.end(), w, w + 4);
+                    ids.push_back((uint16_t)out->sph_perm[j]);
+                }
             }
-            ent.insert(ent.end(), w, w + 4);
         }
+        if (k != ne) return;
     }
     out->sph_lds.swap(ent);
     out->sph_lds_id.swap(ids);

@@ -96,13 +96,14 @@ struct CompiledScene {
     std::vector<uint32_t> sph_perm;     // leaf-order index -> sphere id (shading, ties)
     std::vector<BvhNode> sph_nodes;     // 8 octant layouts of sph_layout_nodes nodes each
     uint32_t sph_layout_nodes = 0;
+    uint32_t sph_lds_entries = 0;       // entries per layout of sph_lds (a leaf of c spheres: c)
     std::vector<SphShade> sph_shade;    // by sphere id
     // Compact sphere BVH for LDS: the layouts of octants
     // (+,+,+) and (-,-,-), 16 B per entry: inner node = fp16 box (lo rounded
     // down, hi up) + (escape | 0x80000000); leaf (one sphere) = (c.xyz, r*r)
     // fp32, its sphere id in sph_lds_id.  Empty when the tree does not qualify.
-    std::vector<uint32_t> sph_lds;      // 2 layouts x sph_layout_nodes x 4 words
-    std::vector<uint16_t> sph_lds_id;   // 2 layouts x sph_layout_nodes
+    std::vector<uint32_t> sph_lds;      // 2 layouts x sph_lds_entries x 4 words
+    std::vector<uint16_t> sph_lds_id;   // 2 layouts x sph_lds_entries
     // Box clusters over the pair records: 28 floats each,
     // (u0.xyz, lo0) (u1.xyz, lo1) (u2.xyz, lo2) (hi0, hi1, hi2, flags)
     // (m0, m1, m2, m3) (m4, m5, all, 0) (w0, w1, w2, 0): an oriented box (padded
