@@ -35,10 +35,17 @@ struct MisMat {
     float metallic, roughness;
 };
 
-struct MisHit {   // IntersectionGPU (:14-20) of a Hit
-    f3 p, n, din;  // point, normal, ray direction
-    MisMat m;
+// IntersectionGPU (:14-20) of a Hit: the normal and the material are read
+// from the shading record (staged in LDS) where they are used.
+struct MisHit {
+    f3 p, din;     // point, ray direction
+    uint32_t id;   // triangle
 };
+
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 __device__ __forceinline__ float clamp01(float x) { return fminf(1.0f, fmaxf(0.0f, x)); }
 
@@ -154,6 +161,14 @@ __device__ __forceinline__ MisMat load_mat(const float4* rec) {
     const float4 r1 = rec[1], r2 = rec[2];
     return MisMat{f3{r1.x, r1.y, r1.z}, r1.w, r2.x};
 }
+// (sv.shade: the shading records, staged in LDS with the scene when it fits)
+__device__ __forceinline__ f3 hit_n(const SceneView& sv, const MisHit& x) {
+    const float4 r0 = sv.shade[3 * x.id];
+    return f3{r0.x, r0.y, r0.z};
+}
+__device__ __forceinline__ MisMat hit_m(const SceneView& sv, const MisHit& x) {
+    return load_mat(sv.shade + 3 * x.id);
+}
 
 template <int GEO>
 __device__ __forceinline__ int mis_closest(const SceneView& sv, f3 o, f3 d, float tmax, float* t) {
@@ -166,7 +181,7 @@ __device__ __forceinline__ int mis_closest(const SceneView& sv, f3 o, f3 d, floa
 template <int GEO, bool POWER>
 __device__ __forceinline__ f3 direct_light(const MisParams& P, const SceneView& sv, const MisHit& x,
                                            float ux, float uy, float nS) {
-    const f3 origin = x.p + x.n * 1e-4f;
+    const f3 origin = x.p + hit_n(sv, x) * 1e-4f;
     // directSquareLightRay (:291-313)
     const float sx = (ux - 0.5f) * P.l_width;
     const float sy = (uy - 0.5f) * P.l_depth;
@@ -178,13 +193,15 @@ __device__ __forceinline__ f3 direct_light(const MisParams& P, const SceneView& 
     const f3 L{tl.x / dist, tl.y / dist, tl.z / dist};
     float t;
     const int id = mis_closest<GEO>(sv, origin, L, dist, &t);
-    if (id < 0 || P.mis_shade[3 * id].w == 0.0f) return f3{0.0f, 0.0f, 0.0f};  // not HitLight
+    if (id < 0 || sv.shade[3 * id].w == 0.0f) return f3{0.0f, 0.0f, 0.0f};  // not HitLight
     const float dl_pdf = light_pdf(P, x.p, L);
-    const f3 c = brdf(x.din, x.n, x.m, L);
+    const f3 n = hit_n(sv, x);
+    const MisMat m = hit_m(sv, x);
+    const f3 c = brdf(x.din, n, m, L);
     const f3 Le{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
     if (POWER) {
-        const float cos_pdf = cosine_pdf(x.n, L);
-        const float v_pdf = vndf_pdf(-x.din, x.n, L, x.m.roughness);
+        const float cos_pdf = cosine_pdf(n, L);
+        const float v_pdf = vndf_pdf(-x.din, n, L, m.roughness);
         const float w = power_h(dl_pdf, cos_pdf, v_pdf, nS);
         const f3 a = (c * w) * Le;
         return f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
@@ -203,18 +220,16 @@ __device__ __forceinline__ f3 continue_sample(const MisParams& P, const SceneVie
     float t;
     const int id = mis_closest<GEO>(sv, origin, dir, 1000.0f, &t);
     if (id < 0) return f3{0.0f, 0.0f, 0.0f};
-    const float4* rec = P.mis_shade + 3 * id;
-    const float4 r0 = rec[0];
-    const f3 c = brdf(x.din, x.n, x.m, dir);
+    const float4 r0 = sv.shade[3 * id];
+    const f3 c = brdf(x.din, hit_n(sv, x), hit_m(sv, x), dir);
     if (r0.w != 0.0f) {  // HitLight
         const f3 a = (c * w) * f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
         return f3{a.x / pdf, a.y / pdf, a.z / pdf};
     }
     MisHit y;
     y.p = origin + dir * t;
-    y.n = f3{r0.x, r0.y, r0.z};
     y.din = dir;
-    y.m = load_mat(rec);
+    y.id = (uint32_t)id;
     const f3 q{c.x / pdf, c.y / pdf, c.z / pdf};
     return q * direct_light<GEO, false>(P, sv, y, u2x, u2y, 1.0f);
 }
@@ -232,24 +247,29 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         dl = dl + direct_light<GEO, true>(P, sv, x, u.x, u.y, nS);
     }
     f3 t, b;
-    onb(x.n, &t, &b);
-    const f3 origin = x.p + x.n * 1e-4f;
-    const f3 V = -x.din;
+    onb(hit_n(sv, x), &t, &b);
     for (uint32_t i = 0; i < S; ++i) {  // cosine-hemisphere sampling (:562-591)
         const float4 u = tab[3 * i + 1];
-        const f3 dir = cosine_dir(x.n, t, b, u.x, u.y);
-        const float cos_pdf = cosine_pdf(x.n, dir);
+        const f3 n = hit_n(sv, x);
+        const f3 origin = x.p + n * 1e-4f;
+        const f3 V = -x.din;
+        const f3 dir = cosine_dir(n, t, b, u.x, u.y);
+        const float cos_pdf = cosine_pdf(n, dir);
         const float dl_pdf = light_pdf(P, x.p, dir);
-        const float v_pdf = vndf_pdf(V, x.n, dir, x.m.roughness);
+        const float v_pdf = vndf_pdf(V, n, dir, hit_m(sv, x).roughness);
         const float w = power_h(cos_pdf, dl_pdf, v_pdf, nS);
         cs = cs + continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w);
     }
     const f3 dc = dl + cs;  // (directLight + cosine) + vndf (:624), same order
     for (uint32_t i = 0; i < S; ++i) {  // VNDF sampling (:593-623)
         const float4 u = tab[3 * i + 2];
-        const f3 dir = vndf_dir(V, x.n, t, b, x.m.roughness, u.x, u.y);
-        const float v_pdf = vndf_pdf(V, x.n, dir, x.m.roughness);
-        const float cos_pdf = cosine_pdf(x.n, dir);
+        const f3 n = hit_n(sv, x);
+        const f3 origin = x.p + n * 1e-4f;
+        const f3 V = -x.din;
+        const float rough = hit_m(sv, x).roughness;
+        const f3 dir = vndf_dir(V, n, t, b, rough, u.x, u.y);
+        const float v_pdf = vndf_pdf(V, n, dir, rough);
+        const float cos_pdf = cosine_pdf(n, dir);
         const float dl_pdf = light_pdf(P, x.p, dir);
         const float w = power_h(v_pdf, dl_pdf, cos_pdf, nS);
         vn = vn + continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w);
@@ -261,7 +281,11 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
 }  // namespace
 
 #ifndef RT_MIS_WAVES_PER_EU
-#define RT_MIS_WAVES_PER_EU 5  // box clusters: 4/5/6/7 waves 24.8/24.5/24.4/25.8 ms (pair loop: 3 waves 37.5, 7 waves 27.6, 8 waves 28.5)
+// 4 waves/SIMD: the kernel fits its 120 VGPRs without scratch (HBM traffic
+// 10.3 MB per 800x600 frame = 1.08x the output bytes); 5 waves ran 23.5 ms
+// with 40 spilled VGPRs (467 MB/frame), 6 waves 22.8 ms with 54 (765 MB/frame),
+// 4 waves 24.3 ms
+#define RT_MIS_WAVES_PER_EU 4
 #endif
 template <int GEO>
 __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel(MisParams P) {
@@ -286,8 +310,13 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) lds[k] = src[k];
+        const uint32_t nc4 = GEO == kGeoPairClu ? kCluF4 * P.nC : 0u;
         if (GEO == kGeoPairClu)  // box clusters after the pair records
-            for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
+            for (uint32_t k = threadIdx.x; k < nc4; k += kBlockThreads) lds[ng4 + k] = P.clusters[k];
+        // then the shading records (3 float4 per triangle): read per lane, often
+        for (uint32_t k = threadIdx.x; k < 3u * sv.nT; k += kBlockThreads)
+            lds[ng4 + nc4 + k] = P.mis_shade[k];
+        sv.shade = lds + ng4 + nc4;
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
@@ -298,20 +327,30 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
     }
+    if (GEO == kGeoTriBvh || GEO == kGeoTriGlobal) sv.shade = P.mis_shade;
 
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t j = blockIdx.y * kTile + (wave >> 1) * 8u + (lane >> 3);
-    if (x >= (uint32_t)P.W || j >= P.row_count) return;
-    const uint32_t y = P.row_start + j * P.row_step;
-    const size_t o = (size_t)j * (size_t)P.W + x;
-
+    // pixel of a lane; recomputed from an opaque threadIdx where it is used
+    // (as in rt_kernel.hip), not held across the camera-ray loop
+    auto pixel_of = [&](uint32_t tid, uint32_t& x, uint32_t& j) {
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
+        x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
+        j = blockIdx.y * kTile + (wave >> 1) * 8u + (lane >> 3);
+    };
+    {
+        uint32_t x, j;
+        pixel_of(threadIdx.x, x, j);
+        if (x >= (uint32_t)P.W || j >= P.row_count) return;
+    }
     const f3 cu{P.cam_u[0], P.cam_u[1], P.cam_u[2]}, cv{P.cam_v[0], P.cam_v[1], P.cam_v[2]};
     const f3 cw{P.cam_w[0], P.cam_w[1], P.cam_w[2]};
     const f3 cpos{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
-    const float fx = (float)x, fy = (float)y, fW = (float)P.W, fH = (float)P.H;
+    const float fW = (float)P.W, fH = (float)P.H;
     f3 acc{0.0f, 0.0f, 0.0f};
     for (uint32_t i = 0; i < P.camera_rays; ++i) {  // :652
+        uint32_t x, j;
+        pixel_of(opaque_u32(threadIdx.x), x, j);
+        const uint32_t y = P.row_start + j * P.row_step;
+        const float fx = (float)x, fy = (float)y;
         // hashRandom(index, i) (:71-85); the 800 is the reference's hard-coded width
         const uint32_t sample_id = (y * 800u + x) * i;
         const float jx = mis_unit(mis_hash(x + y * 800u + sample_id));
@@ -324,20 +363,21 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         float t;
         const int id = mis_closest<GEO>(sv, cpos, d, 1000.0f, &t);
         if (id < 0) continue;                               // Miss (:665)
-        const float4* rec = P.mis_shade + 3 * id;
-        const float4 r0 = rec[0];
+        const float4 r0 = sv.shade[3 * id];
         if (r0.w != 0.0f) {                                 // HitLight (:667-671)
             acc = acc + f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
             continue;
         }
         MisHit h;
         h.p = cpos + d * t;
-        h.n = f3{r0.x, r0.y, r0.z};
         h.din = d;
-        h.m = load_mat(rec);
+        h.id = (uint32_t)id;
         acc = acc + mis_shade_hit<GEO>(P, sv, h);           // :674-676
     }
     const float nc = (float)P.camera_rays;
+    uint32_t x, j;
+    pixel_of(opaque_u32(threadIdx.x), x, j);
+    const size_t o = (size_t)j * (size_t)P.W + x;
     if (P.out) P.out[o] = make_float4(acc.x, acc.y, acc.z, nc);  // textBuffer (:705) + count
     if (P.out8) {
         // :688-706: exposure, Reinhard, clamp, gamma 1/2.2, uchar(c * 255)
@@ -354,8 +394,8 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     }
 }
 
-size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {
-    return (size_t)(n_pairs ? kPairF4 * n_pairs : 3u * n_tri) * sizeof(float4);
+size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + shading records
+    return (size_t)((n_pairs ? kPairF4 * n_pairs : 3u * n_tri) + 3u * n_tri) * sizeof(float4);
 }
 
 hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {

@@ -163,6 +163,7 @@ struct SceneView {
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
     const uint4* sent;        // compact sphere BVH entries in LDS (kGeoSphLds), 2 layouts
     const uint16_t* sid;      // sphere id of each entry (leaves)
+    const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
 };
 
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
@@ -382,7 +383,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
     uint32_t idx = (ANY && id >= 0) ? nN : 0u;  // next entry of this lane's walk (nN: done)
     uint32_t leaf = kNone;                      // the parked leaf
     float pb = 0.0f, pdisc = 0.0f;              // its b and discriminant
-    constexpr int ST = ANY ? 24 : 16;
+    [[maybe_unused]] constexpr int ST = ANY ? 24 : 16;
     RT_STAT(ST, 1);
     RT_STAT(ST + 1, __popcll(__ballot(1)));
     for (;;) {
