@@ -12,7 +12,11 @@ import numpy as np
 
 
 def rank_rows(height: int, world: int, rank: int) -> tuple[int, int, int]:
-    """(row_start, row_step, row_count) of ``rank``'s interleaved tile."""
+    """(row_start, row_step, row_count) of ``rank``'s interleaved tile.
+
+    row_count is 0 for a rank past the last row (more ranks than rows); such a
+    rank must skip its render -- RenderParams reads row_count 0 as "every row"
+    -- and join the gather with an empty tile (rt_render_gather does this)."""
     if not 0 <= rank < world:
         raise ValueError("rank out of range")
     count = (height - 1 - rank) // world + 1 if rank < height else 0

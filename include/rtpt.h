@@ -175,7 +175,8 @@ int rt_last_launch(const rt_ctx* ctx, rt_launch_info* info);
 const char* rt_build_sha(void);
 
 /* Diagnostic counters of a -DRT_STATS build of the kernel (reads and clears
- * up to 16 uint64 counters; RT_ERR_STATE in normal builds). */
+ * up to 32 uint64 counters, slots in rt_trace.hpp; RT_ERR_STATE in normal
+ * builds). */
 int rt_debug_stats(rt_ctx* ctx, uint64_t* out, int n);
 
 /* Message of the last failure on ctx (or of the last failed rt_create when

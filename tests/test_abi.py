@@ -101,6 +101,18 @@ def test_scene_layout_uses_shared_edge_pairs():
     assert big["lds_bytes"] == 6 * 112 and big["sphere_bvh_lds_bytes"] == 0 and big["n_sphere_nodes"] == bvh_nodes(5000)
 
 
+def test_portrait_resolution_is_rejected():
+    """The reference computes aspect = float(res.x / res.y) in integers
+    (sampling.metal:132): a portrait frame gives aspect 0 and halfHeight inf.
+    The boundary refuses it with RT_ERR_INVALID_ARG instead (INTEGRATION.md
+    §4, a documented deviation); square and landscape frames are accepted."""
+    with pytest.raises(g.RtError) as e:
+        g.Scene.cornell_box(30, 40).describe()
+    assert e.value.status == 1 and "aspectRatio 0" in str(e.value)
+    assert g.Scene.cornell_box(40, 40).describe()["n_triangles"] == 36
+    assert g.Scene.cornell_box(41, 40).describe()["n_triangles"] == 36
+
+
 def test_library_carries_the_tree_source_hash():
     """librtpt.so was built from exactly these sources (rt_build_sha, compiled
     in by the Makefile from gpuraytracer_amd/srchash.py); the loader refuses a

@@ -220,7 +220,10 @@ def test_full_size_1080p_properties():
 def test_full_frame_1080p_bit_exact_vs_oracle():
     """The headline workload's frame (config 2 geometry, 1920x1080, 3 bounces)
     at 8 spp, every pixel against the C oracle (~17 M samples on 16 host
-    threads): box clusters, Halton tables and 4 lanes per pixel at full size."""
+    threads): box clusters and 4 lanes per pixel at full size.  8 spp is 2
+    rounds per lane, below kHaltonTabMinRounds: the Halton tables are OFF here;
+    the timed configuration with the tables on is checked by
+    test_gpu_configs.py::test_headline_instantiation_*."""
     s = Scene.cornell_box(1920, 1080)
     sd = seed_splitmix(1920, 1080)
     with Renderer(s, seeds=sd) as r:

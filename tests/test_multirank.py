@@ -58,9 +58,10 @@ def _worker(rank, world, port, W, H, spp, result_path):
     start, step, count = rank_rows(H, world, rank)
     rmax = tile_rows_max(H, world)
     tile = torch.zeros((rmax, W, 4), dtype=torch.float32)
-    tile[:count] = torch.from_numpy(
-        oracle_lib.render(scene, seeds, spp * world, 3, row_start=start, row_step=step,
-                          row_count=count, threads=2))
+    if count:  # a rank past the last row renders nothing (row_count 0 means "all rows")
+        tile[:count] = torch.from_numpy(
+            oracle_lib.render(scene, seeds, spp * world, 3, row_start=start, row_step=step,
+                              row_count=count, threads=2))
     gathered = [torch.zeros_like(tile) for _ in range(world)] if rank == 0 else None
     dist.gather(tile, gathered, dst=0)
     if rank == 0:
@@ -69,12 +70,14 @@ def _worker(rank, world, port, W, H, spp, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_equals_single_rank_frame(world, tmp_path):
+@pytest.mark.parametrize("world,H", [(2, 17), (3, 17), (3, 2)])
+def test_gloo_gather_equals_single_rank_frame(world, H, tmp_path):
+    """(3, 2): more ranks than rows -- rank 2 owns no row and still joins the
+    gather with an empty (padded) tile."""
     import oracle_lib
     from gpuraytracer_amd import Scene, seed_splitmix
 
-    W, H, spp = 24, 17, 2
+    W, spp = 24, 2
     out = str(tmp_path / "frame.npy")
     mp.spawn(_worker, args=(world, _free_port(), W, H, spp, out), nprocs=world, join=True)
     frame = np.load(out)

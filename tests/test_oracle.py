@@ -285,29 +285,67 @@ def test_halton_float_digits():
 
 
 def test_halton_low_digit_split_is_the_reference_sum():
-    """T[i mod b^k] continued with the digits of i / b^k is the reference loop
-    (sampling.metal:107-122) bit for bit (numpy float32, same operation order)."""
+    """rt_halton.hpp halton_tab, emulated operation for operation in numpy
+    float32 for every dimension with a table (kTabDigits parsed from the
+    header): the table T[v] (fill_halton_table: k reference steps of v),
+    i / b^k and i mod b^k by one float digit step with n = b^k, then the fixed
+    nd = digits(b, 3^13) float digit steps (f from f_after(b, k)).  Equals the
+    reference loop (sampling.metal:107-122, variable length) bit for bit on a
+    stride of [0, 3^13) and its top index 3^13 - 1."""
+    import re
     f32 = np.float32
-    for b, k in ((3, 7), (5, 4), (7, 3), (11, 2)):
+    src = open(os.path.join(os.path.dirname(GOLDEN), "..", "gpuraytracer_amd", "csrc",
+                            "rt_halton.hpp")).read()
+    K = [int(v) for v in re.search(r"kTabDigits\[24\] = \{([^}]*)\}", src).group(1).split(",")]
+    small_max = int(re.search(r"constexpr uint32_t kSmallIndexMax = (\d+);", src).group(1))
+    assert small_max == 3 ** 13
+    primes = [2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73,
+              79, 83, 89]
+
+    def recip_up(n):
+        c = f32(1) / f32(n)
+        return np.nextafter(c, f32(2)) if float(c) * n < 1.0 else c
+
+    def digit_step(x, n):  # q = floor(x * c), digit = fma(q, -n, x): exact integers
+        q = np.floor(x * recip_up(n)).astype(f32)
+        return q, (x.astype(np.float64) - q.astype(np.float64) * n).astype(f32)
+
+    i = np.unique(np.concatenate([np.arange(0, small_max, 97), [small_max - 1],
+                                  np.random.default_rng(5).integers(0, small_max, 20000)]))
+    dims = [d for d in range(24) if K[d] > 0]
+    assert dims == [1, 2, 3, 4, 5, 7, 8, 9, 10]
+    for d in dims:
+        b, k = primes[d], K[d]
         inv = f32(1) / f32(b)
-        idx = np.random.default_rng(b).integers(0, 1 << 21, 4000, dtype=np.int64)
-        for i0 in idx:
-            ref_f, ref_r, i = f32(1), f32(0), int(i0)
-            while i > 0:
-                ref_f = f32(ref_f * inv)
-                ref_r = f32(ref_r + f32(ref_f * f32(i % b)))
-                i //= b
-            v, f, r = int(i0) % b ** k, f32(1), f32(0)
-            for _ in range(k):
-                f = f32(f * inv)
-                r = f32(r + f32(f * f32(v % b)))
-                v //= b
-            i = int(i0) // b ** k
-            while i > 0:
-                f = f32(f * inv)
-                r = f32(r + f32(f * f32(i % b)))
-                i //= b
-            assert r.tobytes() == ref_r.tobytes(), (b, i0)
+        nd, cap = 0, 1
+        while cap < small_max:
+            cap *= b
+            nd += 1
+        # reference loop, variable length (lanes stop when i reaches 0)
+        ref, f, v = np.zeros(i.shape, f32), f32(1), i.copy()
+        while (v > 0).any():
+            f = f32(f * inv)
+            live = v > 0
+            ref = np.where(live, (ref + (f * (v % b).astype(f32)).astype(f32)).astype(f32), ref)
+            v //= b
+        # the table: T[v] after k steps of v
+        tv = np.arange(b ** k, dtype=np.int64)
+        tab, f = np.zeros(tv.shape, f32), f32(1)
+        for _ in range(k):
+            f = f32(f * inv)
+            tab = (tab + (f * (tv % b).astype(f32)).astype(f32)).astype(f32)
+            tv //= b
+        # halton_tab
+        x, low = digit_step(i.astype(f32), b ** k)
+        r = tab[low.astype(np.int64)]
+        f = f32(1)
+        for _ in range(k):
+            f = f32(f * inv)  # f_after(b, k)
+        for _ in range(k, nd):
+            f = f32(f * inv)
+            x, dig = digit_step(x, b)
+            r = (r + (f * dig).astype(f32)).astype(f32)
+        assert np.array_equal(r.view(np.uint32), ref.view(np.uint32)), (d, b)
 
 
 # ---- MIS integrator (Sources/gpuRaytracer/shaders.metal) ----------------------------
