@@ -374,6 +374,9 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
                                                 uint32_t nT, f3 o, f3 d, float tmin, float& best,
                                                 int& id) {
     constexpr uint32_t kNone = 0xFFFFFFFFu;
+#ifdef RT_TIMING_NO_SPH_WALK  // timing-only experiment (share of the walks), NOT exact
+    return;
+#endif
     const float a = dot(d, d);
     const float a4 = 4.0f * a;
     const RayBox rb = ray_box(o, d);
