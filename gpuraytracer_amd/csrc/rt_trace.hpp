@@ -166,6 +166,54 @@ struct SceneView {
     const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
 };
 
+// min / max of the culling tests, issued directly.  fminf/fmaxf lower to
+// v_min/v_max_f32 plus a v_max_f32 x,x "canonicalize" of every operand the
+// compiler cannot prove canonical (loads, values through phis: the
+// loop-carried best, the branch-merged slab terms) -- 8 extra VALU per box
+// cluster and 2 per BVH step.  The operands here are results of arithmetic on
+// finite scene data (no signalling NaNs), for which v_min/v_max_f32 return
+// exactly fminf/fmaxf; and these values only decide what is culled, never a
+// result.
+#ifndef RT_ASM_MINMAX
+#define RT_ASM_MINMAX 1
+#endif
+__device__ __forceinline__ float vmin(float a, float b) {
+#if RT_ASM_MINMAX
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fminf(a, b);
+#endif
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+#if RT_ASM_MINMAX
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmaxf(a, b);
+#endif
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+#if RT_ASM_MINMAX
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return fminf(fminf(a, b), c);
+#endif
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+#if RT_ASM_MINMAX
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return fmaxf(fmaxf(a, b), c);
+#endif
+}
+
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
 // node boxes carry the culling margin, so only speed depends on its rounding.
 struct RayBox {
@@ -190,8 +238,8 @@ __device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, con
     const float tx0 = fmaf(n0.x, rb.invd.x, -rb.oinv.x), tx1 = fmaf(n1.x, rb.invd.x, -rb.oinv.x);
     const float ty0 = fmaf(n0.y, rb.invd.y, -rb.oinv.y), ty1 = fmaf(n1.y, rb.invd.y, -rb.oinv.y);
     const float tz0 = fmaf(n0.z, rb.invd.z, -rb.oinv.z), tz1 = fmaf(n1.z, rb.invd.z, -rb.oinv.z);
-    const float tnear = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-    const float tfar = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+    const float tnear = vmax3(vmin(tx0, tx1), vmin(ty0, ty1), vmax(vmin(tz0, tz1), tmin));
+    const float tfar = vmin3(vmax(tx0, tx1), vmax(ty0, ty1), vmin(vmax(tz0, tz1), tmax));
     return tnear <= tfar;
 }
 
@@ -627,11 +675,11 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
                 t0 = (A.w - oa) * ida[a];
                 t1 = (hi[a] - oa) * ida[a];
             }
-            en[a] = fminf(t0, t1);
-            ex[a] = fmaxf(t0, t1);
+            en[a] = vmin(t0, t1);
+            ex[a] = vmax(t0, t1);
         }
-        const float tlo0 = fmaxf(fmaxf(en[0], en[1]), fmaxf(en[2], tmin));
-        const float thi0 = fminf(fminf(ex[0], ex[1]), fminf(ex[2], tmax));
+        const float tlo0 = vmax3(en[0], en[1], vmax(en[2], tmin));
+        const float thi0 = vmin3(ex[0], ex[1], vmin(ex[2], tmax));
         const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
 #ifndef RT_NO_CLU_WAVE_SKIP
         if (!__builtin_amdgcn_ballot_w64(tlo <= thi)) continue;  // no lane meets the box
@@ -673,8 +721,8 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
                 t0 = (A[a].w - oa) * ida;
                 t1 = (hi[a] - oa) * ida;
             }
-            tlo0 = fmaxf(tlo0, fminf(t0, t1));
-            thi0 = fminf(thi0, fmaxf(t0, t1));
+            tlo0 = vmax(tlo0, vmin(t0, t1));
+            thi0 = vmin(thi0, vmax(t0, t1));
         }
         const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
         mask |= (tlo <= thi) ? __float_as_uint(r[5].z) : 0u;
