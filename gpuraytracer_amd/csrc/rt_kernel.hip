@@ -418,13 +418,16 @@ void path_trace_kernel(KParams P) {
     // still interleave over the XCDs, which keeps the cheap and the expensive
     // image regions evenly spread (contiguous bands per XCD ran 7 % slower).
     // Speed only: every tile is rendered exactly once.
+#ifndef RT_XCD_RUN
+#define RT_XCD_RUN 4  // 0: plain dispatch order
+#endif
     uint32_t bx, by;
     {
-        constexpr uint32_t kXcdRun = 4u;
-        const uint32_t n = gridDim.x * gridDim.y, full = n / (8u * kXcdRun) * (8u * kXcdRun);
+        constexpr uint32_t kXcdRun = RT_XCD_RUN;
+        const uint32_t n = gridDim.x * gridDim.y, full = n / (8u * kXcdRun + (kXcdRun == 0)) * (8u * kXcdRun);
         const uint32_t p = blockIdx.y * gridDim.x + blockIdx.x;
         uint32_t t = p;
-        if (p < full) {
+        if (kXcdRun > 0 && p < full) {
             const uint32_t xcd = p % 8u, k = p / 8u;
             t = ((k / kXcdRun) * 8u + xcd) * kXcdRun + k % kXcdRun;
         }
@@ -440,9 +443,13 @@ void path_trace_kernel(KParams P) {
     // opaque copy of threadIdx.x where they are used, and the seed is kept in
     // LDS: otherwise the compiler hoists them out of the sample loop and spills
     // them to scratch for the whole launch (36 B/lane of scratch writes).
+    // Only for the box-cluster and LDS-sphere kernels: the triangle-BVH walk
+    // kernel (global-memory nodes) ran 16 % slower with the opaque copies
+    // (325 vs 281 ms, 10k triangles) and spills about as much without them.
+    constexpr bool kRemat = GEO == kGeoPairClu || GEO == kGeoSphLds;
     auto opaque_tid = []() {
         uint32_t t = threadIdx.x;
-        asm volatile("" : "+v"(t));
+        if constexpr (kRemat) asm volatile("" : "+v"(t));
         return t;
     };
     {
