@@ -417,9 +417,6 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
 // visited in the same order and every value is sph_test's, ranked by (t, id):
 // the same result.  ANY: *id becomes >= 0 on the first accepted hit (and that
 // lane stops).
-#ifndef RT_SPH_PARK_Q
-#define RT_SPH_PARK_Q 2  // roots run once the parked lanes are >= Q/4 of the live ones
-#endif
 template <bool ANY>
 __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t* ids, uint32_t nN,
                                                 uint32_t nT, f3 o, f3 d, float tmin, float& best,
@@ -466,7 +463,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             }
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < nN || leaf != kNone));
-            if (4 * parked >= RT_SPH_PARK_Q * live) break;
+            if (2 * parked >= live) break;
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
         RT_STAT(ST + 5, 1);
