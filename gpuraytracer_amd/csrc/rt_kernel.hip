@@ -627,11 +627,13 @@ namespace {
 // Lanes per pixel (measured on one GPU's share of the N-GPU weak-scaling frame,
 // tools/bench_share.py): 4 for ~1 M pixels and more (also +6 % on the whole
 // 1080p frame: 4x4-pixel waves, more lanes in flight), 16 below that (one GPU's
-// share at N = 4 and 8), never more than spp.
-inline int lanes_per_pixel(const KParams& P) {
+// share at N = 4 and 8), never more than spp.  The LDS sphere-walk kernel
+// takes 16 at every size (measured on config 4, the whole 1080p frame: 198.4 ms
+// at 16 lanes, 204.8 at 4, 227.6 at 1).
+inline int lanes_per_pixel(const KParams& P, int geo) {
     if (P.lanes == 1 || P.lanes == 4 || P.lanes == 16) return P.spp >= P.lanes ? (int)P.lanes : 1;
     const uint64_t px = (uint64_t)P.W * P.row_count;
-    const int want = px >= 1000000ull ? 4 : 16;
+    const int want = (px >= 1000000ull && geo != kGeoSphLds) ? 4 : 16;
     if (P.spp >= (uint32_t)want) return want;
     return P.spp >= 4 ? 4 : 1;
 }
@@ -685,7 +687,7 @@ hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
 template <int B, int GEO, bool SPH, bool SMALL>
 hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     if (SMALL) {
-        const int lpp = lanes_per_pixel(P);
+        const int lpp = lanes_per_pixel(P, GEO);
         if (lpp == 16) return launch_tl<B, GEO, SPH, SMALL, 16>(P, lds_bytes, stream);
         if (lpp == 4) return launch_tl<B, GEO, SPH, SMALL, 4>(P, lds_bytes, stream);
     }

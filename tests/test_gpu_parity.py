@@ -242,6 +242,22 @@ def test_spheres_frame_bit_exact_vs_oracle():
     assert_parity(out, ref, "spheres 240x135 x 8 spp")
 
 
+def test_spheres_16_lanes_frame_and_rows_bit_exact_vs_oracle():
+    """The config-4 launch shape: the LDS sphere-walk kernel takes 16 lanes per
+    pixel whenever spp >= 16 (rt_kernel.hip lanes_per_pixel), whole frame and
+    interleaved rows (one GPU's share of a multi-GPU frame)."""
+    s = Scene.random_spheres(64, 40, 1000, seed=42)
+    sd = seed_splitmix(64, 40)
+    with Renderer(s, seeds=sd) as r:
+        full = r.render(RenderParams(spp=20, bounces=3))
+        assert r.last_launch()["lanes_per_pixel"] == 16
+        assert "<3, 7, true, true, 16>" in r.last_launch()["kernel"]
+        tile = r.render(RenderParams(spp=20, bounces=3, row_start=3, row_step=8))
+    ref = oracle_lib.render(s, sd, 20, 3, threads=16)
+    assert_parity(full, ref, "spheres 64x40 x 20 spp, 16 lanes")
+    assert_parity(tile, ref[3::8], "spheres rows 3::8, 16 lanes")
+
+
 def test_errors_are_status_codes():
     s = Scene.cornell_box(16, 8)
     with Renderer(s) as r:
