@@ -45,7 +45,7 @@ VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
 BYTES_PER_PIXEL = 4 + 16       # seed read (u32) + rgba32F store, per launch
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=150,
@@ -66,16 +66,28 @@ def parse():
                     help="oracle threads (default: every CPU this process may use: its "
                          "affinity, capped by the cgroup CPU quota)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def spawn_ranks(n: int) -> int:
+def visible_gpus() -> int:
+    """GPUs a rank could open, counted WITHOUT initialising HIP in this process
+    (the launcher must stay GPU-free: its children are the ranks).  The count
+    runs in a short-lived child interpreter (torch.cuda.device_count there may
+    initialise HIP; that child exits before any rank starts)."""
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (IndexError, ValueError):
+        raise SystemExit(f"could not count GPUs: {r.stderr.strip()[-400:]}")
+
+
+def spawn_ranks(n: int, argv=None, count_gpus=visible_gpus) -> int:
     """`--gpus N` outside torchrun: start N ranks of this script as child
     processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), before any GPU call in
     this process, and return the worst exit status."""
     import socket
-    import torch
-    have = torch.cuda.device_count()  # counts devices without initialising HIP
+    have = count_gpus()
     if have < n:
         raise SystemExit(f"--gpus {n}: only {have} GPU(s) visible")
     with socket.socket() as s:
@@ -85,11 +97,51 @@ def spawn_ranks(n: int) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] +
+                                      list(sys.argv[1:] if argv is None else argv), env=env))
     rcs = [p.wait() for p in procs]
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
+
+
+class CudaBackend:
+    """The GPU touchpoints of the bench: device, frame tensor, stream, HIP
+    events (torch.cuda.Event on the stream the kernel is launched on), sync and
+    the renderer (librtpt.so through the C-ABI).  tests/test_bench_glue.py
+    swaps in a CPU stand-in to exercise the multi-rank glue with gloo."""
+
+    def __init__(self, local: int):
+        import torch
+        self.torch = torch
+        torch.cuda.set_device(local)
+        self.device = torch.device("cuda", local)
+        self.local = local
+
+    def renderer(self, scene):
+        from gpuraytracer_amd import Renderer
+        return Renderer(scene, device=self.local)
+
+    def comm_unique_id(self) -> bytes:
+        from gpuraytracer_amd import comm_unique_id
+        return comm_unique_id()
+
+    def empty_frame(self, H, W):
+        return self.torch.empty((H, W, 4), dtype=self.torch.float32, device=self.device)
+
+    def stream(self):
+        return self.torch.cuda.current_stream()
+
+    def event(self):
+        return self.torch.cuda.Event(enable_timing=True)
+
+    def synchronize(self):
+        self.torch.cuda.synchronize()
+
+
+def gather_check_rows(H: int, world: int):
+    """Rows rank 0 re-renders locally after an N > 1 run: the first row of
+    every rank's tile and the last row of the frame."""
+    return sorted(set(range(min(world, H))) | {H - 1})
 
 
 def load_profile_json(name):
@@ -186,13 +238,13 @@ def cpu_baseline(scene, width, height, spp, bounces, threads, seconds, gpu_frame
             "timed_frame_rows_checked": (height - 1) // step + 1}
 
 
-def main():
-    args = parse()
+def main(argv=None, backend_factory=CudaBackend):
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, argv))
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
     import torch
@@ -200,10 +252,9 @@ def main():
 
     if world > 1:  # CPU plumbing only: comm id, barriers, max over ranks
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    be = backend_factory(local)
 
-    from gpuraytracer_amd import RenderParams, Renderer, Scene, comm_unique_id
+    from gpuraytracer_amd import RenderParams, Scene
 
     W, H = args.width, args.height
     if args.scene == "cornell":
@@ -217,16 +268,24 @@ def main():
     else:
         scene = Scene.random_triangles(W, H, args.triangles, seed=7)
         workload = f"triangles{args.triangles}_{W}x{H}_{args.spp}spp_b{args.bounces}"
-    renderer = Renderer(scene, device=local)
+    renderer = be.renderer(scene)
+    comm = None
     if world > 1:
-        ids = [comm_unique_id() if rank == 0 else None]
+        ids = [be.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
         renderer.comm_init(rank, world, ids[0])
+        # what RCCL itself counts (ncclCommCount / ncclCommUserRank), from every rank
+        mine = torch.tensor(list(renderer.comm_info()) + [rank], dtype=torch.int64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        comm = {"comm_ranks": int(allr[0][0]),
+                "comm_ranks_consistent": all(int(a[0]) == world and int(a[1]) == int(a[2])
+                                             for a in allr)}
     spp = args.spp * world  # weak scaling: W*H*spp samples per GPU whatever N
     rows = (H - 1 - rank) // world + 1 if rank < H else 0  # this rank's interleaved rows
-    frame = torch.empty((H, W, 4), dtype=torch.float32, device=device) if rank == 0 else None
+    frame = be.empty_frame(H, W) if rank == 0 else None
     params = RenderParams(spp=spp, bounces=args.bounces)
-    stream = torch.cuda.current_stream()
+    stream = be.stream()
 
     def step(evs=None):
         if evs is not None:
@@ -242,15 +301,14 @@ def main():
             evs[1].record(stream)
 
     def barrier():
-        torch.cuda.synchronize()
+        be.synchronize()
         if world > 1:
             dist.barrier()
 
     for _ in range(args.warmup):
         step()
     launch = renderer.last_launch()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    events = [(be.event(), be.event()) for _ in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -259,10 +317,17 @@ def main():
     elapsed = time.perf_counter() - t0
     # HIP events on the stream the kernel runs on, around every timed step: at
     # N = 1 a step is exactly one kernel launch (or the launches of one
-    # progressive frame); at N > 1 it also holds the gather, and the kernel
-    # alone is the last launch's own events (rt_last_kernel_ms)
+    # progressive frame).  At N > 1 a step also holds the gather: the kernel
+    # alone is the one launch's own events (rt_last_kernel_ms), except in
+    # progressive mode, where a step has several launches and the whole step
+    # (render + gather) is the time basis.
     step_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    kernel_ms = step_ms if world == 1 else renderer.last_kernel_ms()
+    if world == 1:
+        kernel_ms, basis = step_ms, "kernel launches of one step (HIP events)"
+    elif args.batch_spp:
+        kernel_ms, basis = step_ms, "whole step: every progressive launch + the gather (HIP events)"
+    else:
+        kernel_ms, basis = renderer.last_kernel_ms(), "the render launch of the last step (HIP events)"
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms, step_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -272,6 +337,17 @@ def main():
 
     if rank == 0:
         frame_ok = bool(torch.isfinite(frame).all().item()) and bool((frame[..., 3] == 1).all().item())
+        gather_check = None
+        if world > 1:
+            # placement proof: rows of every rank's tile, re-rendered here by
+            # one local rt_render each, must equal the gathered frame bit for bit
+            host = frame.cpu().numpy()
+            check = gather_check_rows(H, world)
+            same = all(np.array_equal(
+                renderer.render(RenderParams(spp=spp, bounces=args.bounces, row_start=y,
+                                             row_count=1))[0].view(np.uint32),
+                host[y].view(np.uint32)) for y in check)
+            gather_check = {"rows": check, "bit_exact_vs_local_render": bool(same)}
         total_samples = W * H * spp * args.steps  # all ranks together
         value = total_samples / elapsed / 1e6
         launch_bytes = W * rows * BYTES_PER_PIXEL
@@ -323,6 +399,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": launch["kernel"], "kernel_ms": round(kernel_s * 1e3, 4),
+                         "kernel_ms_basis": basis,
                          "algorithmic_bytes_per_launch": launch_bytes},
             "compute_roofline": compute,
             "launch": launch,
@@ -332,6 +409,9 @@ def main():
             "frame_ok": frame_ok,
             "cpu_baseline": None,
         }
+        if comm is not None:
+            out.update(comm)
+            out["gather_check"] = gather_check
         if world == 1 and args.cpu_baseline != "off":
             # every CPU this process may run on at once: the affinity mask,
             # capped by the cgroup CPU quota (oversubscribing a 16-CPU quota

@@ -19,10 +19,11 @@ from __future__ import annotations
 from ._native import (ABI_VERSION, CameraGPU, MaterialGPU, RtError, SphereGPU,
                       SquareLightGPU, float3, lib, library_path)
 from .host import (DEFAULT_SEED_KEY, MisParams, RenderParams, Renderer, Scene, comm_unique_id,
-                   seed_splitmix, tonemap_rgba8)
+                   place_tiles_host, seed_splitmix, tile_layout, tonemap_rgba8)
 
 __all__ = [
     "ABI_VERSION", "CameraGPU", "MaterialGPU", "SphereGPU", "SquareLightGPU", "float3",
     "RtError", "lib", "library_path", "Scene", "Renderer", "RenderParams", "MisParams",
-    "DEFAULT_SEED_KEY", "seed_splitmix", "tonemap_rgba8", "comm_unique_id",
+    "DEFAULT_SEED_KEY", "seed_splitmix", "tonemap_rgba8", "comm_unique_id", "tile_layout",
+    "place_tiles_host",
 ]

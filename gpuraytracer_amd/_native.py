@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTPT_LIB overrides the in-tree library (A/B builds of the kernel).
 library_path = os.environ.get("RTPT_LIB") or os.path.join(_HERE, "librtpt.so")
@@ -109,6 +109,11 @@ class LaunchInfo(ctypes.Structure):  # rt_launch_info
         return d
 
 
+class TileLayout(ctypes.Structure):  # rt_tile_layout_info
+    _fields_ = [("rows", ctypes.c_uint32), ("rows_max", ctypes.c_uint32),
+                ("row_bytes", ctypes.c_uint64), ("tile_bytes", ctypes.c_uint64)]
+
+
 class MisParamsC(ctypes.Structure):  # rt_mis_params
     _fields_ = [(n, ctypes.c_uint32) for n in
                 ("camera_rays", "mis_samples", "row_start", "row_step", "row_count", "flags")]
@@ -128,6 +133,12 @@ SIGNATURES = {
     "rt_comm_unique_id": (ctypes.c_int, [_P]),
     "rt_comm_init": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P]),
     "rt_render_gather": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),
+    "rt_comm_info": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+    "rt_tile_layout": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_uint32, ctypes.POINTER(TileLayout)]),
+    "rt_place_tiles": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_uint32, _P, _P]),
+    "rt_place_tiles_host": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_uint32, _P]),
     "rt_build_sha": (ctypes.c_char_p, []),
     "rt_debug_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "rt_last_error": (ctypes.c_char_p, [_P]),
@@ -206,11 +217,17 @@ def _load():
     if handle.rt_abi_version() != ABI_VERSION:
         raise ImportError(f"librtpt.so ABI {handle.rt_abi_version()} != {ABI_VERSION}")
     if not os.environ.get("RTPT_LIB"):  # A/B builds (RTPT_LIB) are checked by their maker
-        from .srchash import kernel_source_sha
-        built, tree = handle.rt_build_sha().decode(), kernel_source_sha()
-        if built != tree:
+        from .srchash import have_sources, kernel_source_sha
+        built = handle.rt_build_sha().decode()
+        if not have_sources() or built == "unknown":
+            # installed without its sources, or built outside the Makefile:
+            # nothing to compare against
+            import warnings
+            warnings.warn(f"{library_path}: source hash not checked (library hash {built!r}, "
+                          f"sources {'present' if have_sources() else 'absent'})")
+        elif built != kernel_source_sha():
             raise ImportError(f"{library_path} was built from other sources (hash {built}, "
-                              f"tree {tree}): rebuild it with `make`")
+                              f"tree {kernel_source_sha()}): rebuild it with `make`")
     return handle
 
 

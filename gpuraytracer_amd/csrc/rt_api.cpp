@@ -65,6 +65,8 @@ struct rt_ctx {
     size_t tile_cap = 0;
     void* d_gather = nullptr;   // rank 0: world x rows_max x W pixels
     size_t gather_cap = 0;
+    hipEvent_t ev_tiles = nullptr;  // end of the last gather's reads of d_tile / d_gather
+    bool tiles_pending = false;
     uint32_t lanes = 0;  // RTPT_LANES=1|4|16: lanes per pixel (tuning knob; 0 = auto)
     rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|pairsmem|sorted|bvh (tuning knob)
     std::string err;
@@ -113,6 +115,7 @@ hipError_t upload(T** dptr, const void* src, size_t bytes, hipStream_t s) {
 void release(rt_ctx* c) {
     if (!c) return;
     DeviceGuard g(c->device);
+    if (c->tiles_pending) (void)hipEventSynchronize(c->ev_tiles);  // a gather may still read d_tile
     (void)hipFree(c->d_tri_isect);
     (void)hipFree(c->d_tri_shade);
     (void)hipFree(c->d_pair_isect);
@@ -135,6 +138,7 @@ void release(rt_ctx* c) {
     if (c->comm) (void)ncclCommDestroy(c->comm);
     (void)hipFree(c->d_tile);
     (void)hipFree(c->d_gather);
+    if (c->ev_tiles) (void)hipEventDestroy(c->ev_tiles);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -299,9 +303,44 @@ size_t pixel_bytes(uint32_t flags) {
     return (flags & RT_OUT_RGBA8) ? 4u : (flags & RT_OUT_FP16) ? 8u : 16u;
 }
 
+// Row layout of the gather (rt_tile_layout): rank k of N owns the frame rows
+// y = k + j*N, j < rows; every rank sends a tile padded to rows_max rows, so
+// the gathered buffer holds N tiles of tile_bytes back to back.  A rank past
+// the last row (N > H) owns no row and sends its padded tile all the same.
+struct TileLayout {
+    uint32_t rows, rows_max;
+    size_t row_bytes, tile_bytes;
+};
+
+TileLayout tile_layout(uint32_t W, uint32_t H, uint32_t N, uint32_t rank, uint32_t flags) {
+    TileLayout L;
+    L.rows = rank < H ? (H - 1u - rank) / N + 1u : 0u;
+    L.rows_max = (H + N - 1u) / N;
+    L.row_bytes = (size_t)W * pixel_bytes(flags);
+    L.tile_bytes = (size_t)L.rows_max * L.row_bytes;
+    return L;
+}
+
+bool tile_args_ok(int32_t W, int32_t H, int32_t N) { return W > 0 && H > 0 && N > 0; }
+
+// Rank 0's placement after the gather: tile row j of rank k -> frame row
+// k + j*N, one strided copy per rank (device or host frame by RT_OUT_DEVICE).
+hipError_t place_tiles_dev(const void* gathered, uint32_t W, uint32_t H, uint32_t N, uint32_t flags,
+                           void* frame, hipStream_t stream) {
+    const bool dev = (flags & RT_OUT_DEVICE) != 0;
+    for (uint32_t k = 0; k < N && k < H; ++k) {
+        const TileLayout L = tile_layout(W, H, N, k, flags);
+        const hipError_t e = hipMemcpy2DAsync(static_cast<char*>(frame) + k * L.row_bytes, N * L.row_bytes,
+                                              static_cast<const char*>(gathered) + k * L.tile_bytes,
+                                              L.row_bytes, L.row_bytes, L.rows,
+                                              dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 // rt_render_gather: this rank's interleaved rows into d_tile, one ncclGather of
-// the (padded, equal-sized) tiles to rank 0, then one strided copy per rank
-// that puts tile row j of rank k at frame row k + j*world.
+// the (padded, equal-sized) tiles to rank 0, then place_tiles_dev.
 int render_gather_impl(rt_ctx* c, const rt_render_params* p, void* frame, hipStream_t stream) {
     if (!p) return fail(c, RT_ERR_INVALID_ARG, "params is null");
     if (!c->comm) return fail(c, RT_ERR_STATE, "no communicator (rt_comm_init)");
@@ -309,45 +348,43 @@ int render_gather_impl(rt_ctx* c, const rt_render_params* p, void* frame, hipStr
         return fail(c, RT_ERR_INVALID_ARG, "rt_render_gather partitions the rows itself: "
                                            "params must name the whole frame (row_start 0, "
                                            "row_step 0 or 1, row_count 0)");
+    if ((p->flags & RT_OUT_FP16) && (p->flags & RT_OUT_RGBA8))
+        return fail(c, RT_ERR_INVALID_ARG, "RT_OUT_FP16 and RT_OUT_RGBA8 are exclusive");
     const bool want_out = !(p->flags & RT_OUT_NONE);
     const bool dev = (p->flags & RT_OUT_DEVICE) != 0;
     if (want_out && c->rank == 0 && !frame) return fail(c, RT_ERR_INVALID_ARG, "frame is null on rank 0");
     const uint32_t H = (uint32_t)c->scene.cam.H, W = (uint32_t)c->scene.cam.W, N = (uint32_t)c->world;
-    const uint32_t rows_max = (H + N - 1) / N;
-    const uint32_t mine = (uint32_t)c->rank < H ? (H - 1u - (uint32_t)c->rank) / N + 1u : 0u;
-    const size_t px = pixel_bytes(p->flags);
-    const size_t tile_bytes = (size_t)rows_max * W * px;
+    const TileLayout L = tile_layout(W, H, N, (uint32_t)c->rank, p->flags);
+    hipError_t e;
+    // d_tile / d_gather are reused: a previous call on another stream may still
+    // be gathering from them (RT_OUT_DEVICE returns without a host sync)
+    if (c->tiles_pending && (e = hipStreamWaitEvent(stream, c->ev_tiles, 0)) != hipSuccess)
+        return hip_fail(c, RT_ERR_LAUNCH, "hipStreamWaitEvent(previous gather)", e);
     int st;
-    if (want_out && (st = ensure_staging(c, &c->d_tile, &c->tile_cap, tile_bytes, "hipMalloc(tile)")) != RT_OK)
+    if (want_out && (st = ensure_staging(c, &c->d_tile, &c->tile_cap, L.tile_bytes, "hipMalloc(tile)")) != RT_OK)
         return st;
-    if (mine > 0) {  // a rank past the last row renders nothing but still joins the gather
+    if (L.rows > 0) {  // a rank past the last row renders nothing but still joins the gather
         rt_render_params q = *p;
         q.row_start = (uint32_t)c->rank;
         q.row_step = N;
-        q.row_count = mine;
+        q.row_count = L.rows;
         q.flags = p->flags | RT_OUT_DEVICE;
         if ((st = render_impl(c, &q, c->d_tile, true, stream, false)) != RT_OK) return st;
     }
     if (!want_out) return RT_OK;
-    if (c->rank == 0 && (st = ensure_staging(c, &c->d_gather, &c->gather_cap, tile_bytes * N,
+    if (c->rank == 0 && (st = ensure_staging(c, &c->d_gather, &c->gather_cap, L.tile_bytes * N,
                                              "hipMalloc(gather)")) != RT_OK)
         return st;
-    ncclResult_t r = ncclGather(c->d_tile, c->rank == 0 ? c->d_gather : nullptr, tile_bytes, ncclUint8,
+    ncclResult_t r = ncclGather(c->d_tile, c->rank == 0 ? c->d_gather : nullptr, L.tile_bytes, ncclUint8,
                                 0, c->comm, stream);
     if (r != ncclSuccess) return nccl_fail(c, "ncclGather", r);
-    if (c->rank == 0) {
-        const size_t row = (size_t)W * px;
-        for (uint32_t k = 0; k < N && k < H; ++k) {
-            const uint32_t rows_k = (H - 1u - k) / N + 1u;
-            hipError_t e = hipMemcpy2DAsync(static_cast<char*>(frame) + k * row, N * row,
-                                            static_cast<char*>(c->d_gather) + k * tile_bytes, row,
-                                            row, rows_k,
-                                            dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, stream);
-            if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpy2DAsync(frame rows)", e);
-        }
-    }
+    if (c->rank == 0 && (e = place_tiles_dev(c->d_gather, W, H, N, p->flags, frame, stream)) != hipSuccess)
+        return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpy2DAsync(frame rows)", e);
+    if ((e = hipEventRecord(c->ev_tiles, stream)) != hipSuccess)
+        return hip_fail(c, RT_ERR_LAUNCH, "hipEventRecord(gather)", e);
+    c->tiles_pending = true;
     if (!dev) {
-        hipError_t e = hipStreamSynchronize(stream);
+        e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return hip_fail(c, RT_ERR_COMM, "render+gather execution", e);
     }
     return RT_OK;
@@ -566,7 +603,8 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
         if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
             status = RT_ERR_NO_DEVICE; msg = std::string("hipStreamCreate: ") + hipGetErrorString(e); break;
         }
-        if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess) {
+        if ((e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&c->ev_tiles, hipEventDisableTiming)) != hipSuccess) {
             status = RT_ERR_NO_DEVICE; msg = std::string("hipEventCreate: ") + hipGetErrorString(e); break;
         }
         const rt::CompiledScene& s = c->scene;
@@ -706,6 +744,58 @@ int rt_render_gather(rt_ctx* c, const rt_render_params* p, void* frame, void* hi
     DeviceGuard g(c->device);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
     return render_gather_impl(c, p, frame, s);
+}
+
+int rt_comm_info(const rt_ctx* c, int32_t* count, int32_t* rank) {
+    if (!c || !count || !rank) return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
+    if (!c->comm) return RT_ERR_STATE;
+    int n = 0, r = 0;
+    ncclResult_t res = ncclCommCount(c->comm, &n);
+    if (res == ncclSuccess) res = ncclCommUserRank(c->comm, &r);
+    if (res != ncclSuccess) return RT_ERR_COMM;
+    *count = n;
+    *rank = r;
+    return RT_OK;
+}
+
+int rt_tile_layout(int32_t width, int32_t height, int32_t world, int32_t rank, uint32_t flags,
+                   rt_tile_layout_info* out) {
+    if (!out || !tile_args_ok(width, height, world) || rank < 0 || rank >= world)
+        return RT_ERR_INVALID_ARG;
+    const TileLayout L = tile_layout((uint32_t)width, (uint32_t)height, (uint32_t)world, (uint32_t)rank, flags);
+    out->rows = L.rows;
+    out->rows_max = L.rows_max;
+    out->row_bytes = L.row_bytes;
+    out->tile_bytes = L.tile_bytes;
+    return RT_OK;
+}
+
+int rt_place_tiles(rt_ctx* c, const void* gathered_device, int32_t world, uint32_t flags, void* frame,
+                   void* hip_stream) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
+    if (!gathered_device || !frame || world < 1) return fail(c, RT_ERR_INVALID_ARG, "null buffer or world < 1");
+    if ((flags & RT_OUT_FP16) && (flags & RT_OUT_RGBA8))
+        return fail(c, RT_ERR_INVALID_ARG, "RT_OUT_FP16 and RT_OUT_RGBA8 are exclusive");
+    DeviceGuard g(c->device);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipError_t e = place_tiles_dev(gathered_device, (uint32_t)c->scene.cam.W, (uint32_t)c->scene.cam.H,
+                                   (uint32_t)world, flags, frame, s);
+    if (e == hipSuccess && !(flags & RT_OUT_DEVICE)) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "place tiles", e);
+    return RT_OK;
+}
+
+int rt_place_tiles_host(const void* gathered, int32_t width, int32_t height, int32_t world, uint32_t flags,
+                        void* frame) {
+    if (!gathered || !frame || !tile_args_ok(width, height, world)) return RT_ERR_INVALID_ARG;
+    const uint32_t W = (uint32_t)width, H = (uint32_t)height, N = (uint32_t)world;
+    for (uint32_t k = 0; k < N && k < H; ++k) {
+        const TileLayout L = tile_layout(W, H, N, k, flags);
+        for (uint32_t j = 0; j < L.rows; ++j)
+            memcpy(static_cast<char*>(frame) + (size_t)(k + j * N) * L.row_bytes,
+                   static_cast<const char*>(gathered) + k * L.tile_bytes + j * L.row_bytes, L.row_bytes);
+    }
+    return RT_OK;
 }
 
 int rt_last_launch(const rt_ctx* c, rt_launch_info* info) {

@@ -432,7 +432,6 @@ static void build_sphere_lds(CompiledScene* out) {
     }
     const uint32_t ne = pos[nn];  // the same in every layout (a permutation of the same nodes)
     if (ne > 0x7FFFu) return;
-    out->sph_lds_entries = ne;
     std::vector<uint32_t> ent;
     std::vector<uint16_t> ids;
     for (int oct : {0, 7}) {
@@ -472,8 +471,11 @@ static void build_sphere_lds(CompiledScene* out) {
         }
         if (k != ne) return;
     }
+    // set together, only once every check passed: a nonzero count always
+    // comes with its entries
     out->sph_lds.swap(ent);
     out->sph_lds_id.swap(ids);
+    out->sph_lds_entries = ne;
 }
 
 static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint32_t n,

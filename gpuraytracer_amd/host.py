@@ -20,7 +20,7 @@ import numpy as np
 from ._native import (RT_COMM_ID_BYTES, RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16,
                       RT_OUT_NONE, RT_OUT_RGBA8,
                       CameraGPU, LaunchInfo, MaterialGPU, MisParamsC, RenderParamsC, RtError,
-                      SceneDesc, SceneInfo, SphereGPU, SquareLightGPU, float3, lib)
+                      SceneDesc, SceneInfo, SphereGPU, SquareLightGPU, TileLayout, float3, lib)
 
 DEFAULT_SEED_KEY = 0x5EED00000000
 
@@ -55,6 +55,36 @@ def comm_unique_id() -> bytes:
     buf = (ctypes.c_uint8 * RT_COMM_ID_BYTES)()
     _check(lib.rt_comm_unique_id(buf))
     return bytes(buf)
+
+
+def _pixel_flags(fp16: bool = False, rgba8: bool = False) -> int:
+    return (RT_OUT_FP16 if fp16 else 0) | (RT_OUT_RGBA8 if rgba8 else 0)
+
+
+def tile_layout(width: int, height: int, world: int, rank: int, fp16: bool = False,
+                rgba8: bool = False) -> dict:
+    """rt_tile_layout: rank's rows of the rt_render_gather partition (y = rank +
+    j*world) and the padded tile every rank sends (rows_max, tile_bytes)."""
+    t = TileLayout()
+    _check(lib.rt_tile_layout(width, height, world, rank, _pixel_flags(fp16, rgba8), ctypes.byref(t)))
+    return {k: getattr(t, k) for k, _ in TileLayout._fields_}
+
+
+def place_tiles_host(gathered: np.ndarray, width: int, height: int, world: int) -> np.ndarray:
+    """rt_place_tiles_host: ``gathered`` = ``world`` padded tiles back to back
+    (uint8/uint16/float32 RGBA pixels, any shape with 4 channels last); returns
+    the (height, width, 4) frame rank 0 of rt_render_gather would assemble."""
+    g = np.ascontiguousarray(gathered)
+    fp16, rgba8 = g.dtype == np.uint16, g.dtype == np.uint8
+    if g.dtype not in (np.float32, np.uint16, np.uint8):
+        raise ValueError("gathered pixels must be float32, uint16 (fp16 bits) or uint8")
+    lay = tile_layout(width, height, world, 0, fp16, rgba8)
+    if g.nbytes != world * lay["tile_bytes"]:
+        raise ValueError(f"gathered holds {g.nbytes} bytes, expected {world} x {lay['tile_bytes']}")
+    frame = np.empty((height, width, 4), g.dtype)
+    _check(lib.rt_place_tiles_host(g.ctypes.data_as(ctypes.c_void_p), width, height, world,
+                                   _pixel_flags(fp16, rgba8), frame.ctypes.data_as(ctypes.c_void_p)))
+    return frame
 
 
 class Scene:
@@ -407,6 +437,35 @@ class Renderer:
         ptr = out if isinstance(out, int) else out.data_ptr()
         _check(lib.rt_render_gather(self._ctx, ctypes.byref(p.c(RT_OUT_DEVICE)), ctypes.c_void_p(ptr),
                                     ctypes.c_void_p(stream)), self._ctx)
+        return out
+
+    def comm_info(self) -> tuple[int, int]:
+        """rt_comm_info: (ranks in the communicator, this rank) as RCCL reports them."""
+        n, r = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib.rt_comm_info(self._ctx, ctypes.byref(n), ctypes.byref(r)), self._ctx)
+        return n.value, r.value
+
+    def place_tiles(self, gathered, world: int, out=None, fp16: bool = False, rgba8: bool = False,
+                    stream=None):
+        """rt_place_tiles: rank 0's placement step of rt_render_gather on a device
+        buffer ``gathered`` (``world`` padded tiles back to back).  Returns the
+        host frame, or fills the device tensor ``out`` on ``stream``."""
+        gp = gathered if isinstance(gathered, int) else gathered.data_ptr()
+        flags = _pixel_flags(fp16, rgba8)
+        if out is None:
+            dt = np.uint8 if rgba8 else np.uint16 if fp16 else np.float32
+            frame = np.empty((self.scene.height, self.scene.width, 4), dt)
+            _check(lib.rt_place_tiles(self._ctx, ctypes.c_void_p(gp), world, flags,
+                                      frame.ctypes.data_as(ctypes.c_void_p), None), self._ctx)
+            return frame
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream().cuda_stream
+        elif hasattr(stream, "cuda_stream"):
+            stream = stream.cuda_stream
+        ptr = out if isinstance(out, int) else out.data_ptr()
+        _check(lib.rt_place_tiles(self._ctx, ctypes.c_void_p(gp), world, flags | RT_OUT_DEVICE,
+                                  ctypes.c_void_p(ptr), ctypes.c_void_p(stream)), self._ctx)
         return out
 
     def last_launch(self) -> dict:

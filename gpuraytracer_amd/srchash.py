@@ -11,6 +11,12 @@ import os
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def have_sources() -> bool:
+    """Whether the library's source directories are present (an installed
+    package may ship librtpt.so without them)."""
+    return all(os.path.isdir(os.path.join(_ROOT, sub)) for sub in ("gpuraytracer_amd/csrc", "include"))
+
+
 def kernel_source_sha() -> str:
     h = hashlib.sha256()
     for sub in ("gpuraytracer_amd/csrc", "include"):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RTPT_ABI_VERSION 4
+#define RTPT_ABI_VERSION 5
 
 /* Maximum bounce count: Halton dimensions 2+5b..5+5b must stay inside the
  * 24-entry `primes[]` table (`RTrace/sampling.metal:97-104`); b <= 3. */
@@ -154,6 +154,37 @@ int rt_comm_init(rt_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RT_C
  * running sums) nothing is gathered.  RT_ERR_STATE without rt_comm_init,
  * RT_ERR_COMM when the gather fails. */
 int rt_render_gather(rt_ctx* ctx, const rt_render_params* params, void* frame, void* hip_stream);
+
+/* The communicator as RCCL sees it (ncclCommCount / ncclCommUserRank): lets a
+ * caller prove that N ranks joined.  RT_ERR_STATE without rt_comm_init. */
+int rt_comm_info(const rt_ctx* ctx, int32_t* count, int32_t* rank);
+
+/* Row layout of rt_render_gather (host-only, no device): rank `rank` of
+ * `world` owns rows y = rank + j*world, j < rows; every rank sends a tile
+ * padded to rows_max rows (tile_bytes = rows_max * row_bytes, the ncclGather
+ * count), so rank 0 receives world tiles back to back.  rows is 0 for a rank
+ * past the last row (world > height).  Pixel bytes by flags (16 / 8 / 4). */
+typedef struct rt_tile_layout_info {
+    uint32_t rows;
+    uint32_t rows_max;
+    uint64_t row_bytes;
+    uint64_t tile_bytes;
+} rt_tile_layout_info;
+int rt_tile_layout(int32_t width, int32_t height, int32_t world, int32_t rank, uint32_t flags,
+                   rt_tile_layout_info* out);
+
+/* Rank 0's placement step of rt_render_gather on its own: `gathered_device`
+ * holds `world` tiles of rt_tile_layout's tile_bytes back to back (device
+ * memory); tile row j of rank k lands at frame row k + j*world.  `frame` is
+ * H*W pixels in the format of flags, device memory with RT_OUT_DEVICE
+ * (enqueued on hip_stream, NULL = the context's stream) or host memory (the
+ * call blocks).  The same code rt_render_gather runs after its ncclGather. */
+int rt_place_tiles(rt_ctx* ctx, const void* gathered_device, int32_t world, uint32_t flags,
+                   void* frame, void* hip_stream);
+
+/* The same placement on host memory (no device). */
+int rt_place_tiles_host(const void* gathered, int32_t width, int32_t height, int32_t world,
+                        uint32_t flags, void* frame);
 
 /* Which kernel instantiation the most recent rt_render/rt_render_async
  * launched, with its launch shape: lets a caller (bench, tests) state which

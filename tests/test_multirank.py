@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
+from gpuraytracer_amd import place_tiles_host, tile_layout
 from gpuraytracer_amd.tiles import assemble, rank_rows, tile_rows_max
 
 
@@ -33,6 +34,43 @@ def test_assemble_numpy_roundtrip():
         t[:count] = frame[k::N]
         tiles.append(t)
     assert np.array_equal(assemble(tiles, H), frame)
+
+
+@pytest.mark.parametrize("H", [1, 2, 5, 17, 1080])
+def test_c_abi_tile_layout_matches_partition(H):
+    """rt_tile_layout (the arithmetic rt_render_gather and its placement use)
+    against the Python partition, N in {1, 2, 3, 8, 16}, N > H included."""
+    W = 7
+    for N in (1, 2, 3, 8, 16):
+        for k in range(N):
+            for fp16, rgba8, px in ((False, False, 16), (True, False, 8), (False, True, 4)):
+                lay = tile_layout(W, H, N, k, fp16, rgba8)
+                _, _, count = rank_rows(H, N, k)
+                assert lay["rows"] == count, (H, N, k)
+                assert lay["rows_max"] == tile_rows_max(H, N)
+                assert lay["row_bytes"] == W * px
+                assert lay["tile_bytes"] == tile_rows_max(H, N) * W * px
+
+
+@pytest.mark.parametrize("H", [1, 2, 5, 17, 1080])
+def test_c_abi_place_tiles_host_roundtrip(H):
+    """rt_place_tiles_host (rank 0's placement after the gather, host form):
+    the frame cut into padded interleaved tiles, the padding filled with junk,
+    comes back bit-identical for N in {1, 2, 3, 8, 16} in all pixel formats."""
+    W = 6
+    rng = np.random.default_rng(H)
+    for dt in (np.float32, np.uint16, np.uint8):
+        frame = rng.integers(0, 255, size=(H, W, 4)).astype(dt)
+        for N in (1, 2, 3, 8, 16):
+            rmax = tile_rows_max(H, N)
+            tiles = np.full((N, rmax, W, 4), 0xAB, dt)
+            for k in range(N):
+                _, _, count = rank_rows(H, N, k)
+                tiles[k, :count] = frame[k::N]
+            out = place_tiles_host(tiles, W, H, N)
+            assert np.array_equal(out, frame), (dt, N)
+    with pytest.raises(ValueError):
+        place_tiles_host(np.zeros((3, 2), np.float32), W, H, 2)
 
 
 def _free_port():
@@ -64,8 +102,8 @@ def _worker(rank, world, port, W, H, spp, result_path):
                               row_count=count, threads=2))
     gathered = [torch.zeros_like(tile) for _ in range(world)] if rank == 0 else None
     dist.gather(tile, gathered, dst=0)
-    if rank == 0:
-        np.save(result_path, assemble(gathered, H).numpy())
+    if rank == 0:  # the product's placement code (rt_place_tiles_host)
+        np.save(result_path, place_tiles_host(torch.stack(gathered).numpy(), W, H, world))
     dist.barrier()
     dist.destroy_process_group()
 
