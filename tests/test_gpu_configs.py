@@ -174,3 +174,29 @@ def test_rgba8_device_output_progressive():
         torch.cuda.synchronize()
         ref = oracle_lib.tonemap(r.render(RenderParams(spp=12)))
     assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+C4_KERNEL = "rt::path_trace_kernel<3, 7, true, true, 16>"  # what bench.py --scene spheres times
+
+
+def test_c4_timed_launch_1080p_256spp_bands_vs_oracle():
+    """Config 4 exactly as the bench times it: the whole 1920x1080 frame of the
+    1000-sphere scene at 256 spp in ONE launch (16 lanes per pixel, 16 rounds
+    per lane, 1024-thread workgroups with the compact BVH in LDS, grid
+    240x135).  Three 4-row bands of that frame (top, middle, lower third) are
+    compared with the brute-force oracle bit for bit (5.9 M samples on the
+    host); the whole frame is finite with alpha 1."""
+    W, H = 1920, 1080
+    s = Scene.random_spheres(W, H, 1000, seed=42)
+    sd = seed_splitmix(W, H)
+    with Renderer(s, seeds=sd) as r:
+        frame = r.render(RenderParams(spp=256, bounces=3))
+        info = r.last_launch()
+    assert info["kernel"] == C4_KERNEL, info
+    assert info["lanes_per_pixel"] == 16 and info["block_threads"] == 1024, info
+    assert (info["grid_x"], info["grid_y"]) == (240, 135), info
+    assert info["lds_bytes"] == s.describe()["sphere_bvh_lds_bytes"], info
+    assert np.isfinite(frame).all() and np.all(frame[..., 3] == 1.0)
+    for start in (100, 540, 900):
+        ref = oracle_lib.render(s, sd, 256, 3, row_start=start, row_count=4, threads=16)
+        assert_parity(frame[start:start + 4], ref, f"C4 rows {start}+4 x 256 spp")

@@ -85,7 +85,7 @@ def test_place_tiles_n_ranks_equals_single_frame(H):
     included -- in all three pixel formats, into host and device frames: every
     frame is bit-identical to one rt_render of the whole frame."""
     import torch
-    W, spp = 40, 2
+    W, spp = (1920 if H == 1080 else 40), 2  # W >= H: the reference's integer aspect
     s = Scene.cornell_box(W, H)
     with Renderer(s) as r:
         stream = torch.cuda.current_stream()
