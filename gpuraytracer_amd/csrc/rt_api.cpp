@@ -324,19 +324,31 @@ TileLayout tile_layout(uint32_t W, uint32_t H, uint32_t N, uint32_t rank, uint32
 bool tile_args_ok(int32_t W, int32_t H, int32_t N) { return W > 0 && H > 0 && N > 0; }
 
 // Rank 0's placement after the gather: tile row j of rank k -> frame row
-// k + j*N, one strided copy per rank (device or host frame by RT_OUT_DEVICE).
-hipError_t place_tiles_dev(const void* gathered, uint32_t W, uint32_t H, uint32_t N, uint32_t flags,
-                           void* frame, hipStream_t stream) {
+// k + j*N (rt_kernel.hip place_tiles_kernel, one launch on `stream`).  A host
+// frame is assembled in the context's staging buffer, then copied down once
+// the kernel has finished.
+int place_tiles_impl(rt_ctx* c, const void* gathered, uint32_t N, uint32_t flags, void* frame,
+                     hipStream_t stream) {
+    const uint32_t W = (uint32_t)c->scene.cam.W, H = (uint32_t)c->scene.cam.H;
+    const TileLayout L = tile_layout(W, H, N, 0, flags);
     const bool dev = (flags & RT_OUT_DEVICE) != 0;
-    for (uint32_t k = 0; k < N && k < H; ++k) {
-        const TileLayout L = tile_layout(W, H, N, k, flags);
-        const hipError_t e = hipMemcpy2DAsync(static_cast<char*>(frame) + k * L.row_bytes, N * L.row_bytes,
-                                              static_cast<const char*>(gathered) + k * L.tile_bytes,
-                                              L.row_bytes, L.row_bytes, L.rows,
-                                              dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, stream);
-        if (e != hipSuccess) return e;
+    const size_t frame_bytes = (size_t)H * L.row_bytes;
+    void* dst = frame;
+    int st;
+    if (!dev) {
+        if ((st = ensure_staging(c, &c->d_out, &c->out_cap, frame_bytes, "hipMalloc(frame staging)")) != RT_OK)
+            return st;
+        dst = c->d_out;
     }
-    return hipSuccess;
+    hipError_t e = rt::launch_place_tiles(gathered, dst, L.row_bytes, L.tile_bytes, H, N, stream);
+    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "place_tiles launch", e);
+    if (!dev) {
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(frame, dst, frame_bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream)) != hipSuccess)
+            return hip_fail(c, RT_ERR_LAUNCH, "frame copy to host", e);
+    }
+    return RT_OK;
 }
 
 // rt_render_gather: this rank's interleaved rows into d_tile, one ncclGather of
@@ -378,8 +390,8 @@ int render_gather_impl(rt_ctx* c, const rt_render_params* p, void* frame, hipStr
     ncclResult_t r = ncclGather(c->d_tile, c->rank == 0 ? c->d_gather : nullptr, L.tile_bytes, ncclUint8,
                                 0, c->comm, stream);
     if (r != ncclSuccess) return nccl_fail(c, "ncclGather", r);
-    if (c->rank == 0 && (e = place_tiles_dev(c->d_gather, W, H, N, p->flags, frame, stream)) != hipSuccess)
-        return hip_fail(c, RT_ERR_LAUNCH, "hipMemcpy2DAsync(frame rows)", e);
+    if (c->rank == 0 && (st = place_tiles_impl(c, c->d_gather, N, p->flags, frame, stream)) != RT_OK)
+        return st;
     if ((e = hipEventRecord(c->ev_tiles, stream)) != hipSuccess)
         return hip_fail(c, RT_ERR_LAUNCH, "hipEventRecord(gather)", e);
     c->tiles_pending = true;
@@ -778,11 +790,7 @@ int rt_place_tiles(rt_ctx* c, const void* gathered_device, int32_t world, uint32
         return fail(c, RT_ERR_INVALID_ARG, "RT_OUT_FP16 and RT_OUT_RGBA8 are exclusive");
     DeviceGuard g(c->device);
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-    hipError_t e = place_tiles_dev(gathered_device, (uint32_t)c->scene.cam.W, (uint32_t)c->scene.cam.H,
-                                   (uint32_t)world, flags, frame, s);
-    if (e == hipSuccess && !(flags & RT_OUT_DEVICE)) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "place tiles", e);
-    return RT_OK;
+    return place_tiles_impl(c, gathered_device, (uint32_t)world, flags, frame, s);
 }
 
 int rt_place_tiles_host(const void* gathered, int32_t width, int32_t height, int32_t world, uint32_t flags,

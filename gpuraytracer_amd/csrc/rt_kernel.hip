@@ -622,6 +622,44 @@ __global__ void fill_seeds_kernel(uint32_t* seeds, uint64_t key, uint64_t n) {
     }
 }
 
+// Placement of the gathered row tiles (rt_render_gather / rt_place_tiles): one
+// thread per U-byte unit of the frame, consecutive threads along a row, so the
+// reads (a tile row) and the writes (a frame row) are both coalesced.  A
+// kernel on the caller's stream rather than N strided hipMemcpy2DAsync: a
+// device-to-device 2D copy enqueued on the null stream was measured to start
+// before the kernels enqueued ahead of it had finished (it read the gather
+// buffer's previous contents), and the kernel is one launch whatever N.
+template <typename U>
+__global__ void place_tiles_kernel(const U* __restrict__ gathered, U* __restrict__ frame, uint32_t row_u,
+                                   size_t tile_u, uint32_t H, uint32_t N) {
+    const uint32_t y = blockIdx.y;
+    const uint32_t k = y % N, j = y / N;
+    const U* src = gathered + k * tile_u + (size_t)j * row_u;
+    U* dst = frame + (size_t)y * row_u;
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < row_u; u += gridDim.x * blockDim.x)
+        dst[u] = src[u];
+}
+
+hipError_t launch_place_tiles(const void* gathered, void* frame, size_t row_bytes, size_t tile_bytes,
+                              uint32_t H, uint32_t N, hipStream_t stream) {
+    if (H == 0 || N == 0 || row_bytes == 0) return hipSuccess;
+    if (row_bytes % 4 || tile_bytes % 4 || H > 65535u) return hipErrorInvalidValue;  // grid.y limit
+    const bool wide = row_bytes % 16 == 0 && tile_bytes % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(gathered) % 16 == 0 && reinterpret_cast<uintptr_t>(frame) % 16 == 0;
+    const size_t unit = wide ? 16 : 4;
+    const uint32_t row_u = (uint32_t)(row_bytes / unit);
+    const dim3 grid((row_u + 255u) / 256u, H);
+    if (wide)
+        hipLaunchKernelGGL(place_tiles_kernel<uint4>, grid, dim3(256), 0, stream,
+                           static_cast<const uint4*>(gathered), static_cast<uint4*>(frame), row_u,
+                           tile_bytes / 16, H, N);
+    else
+        hipLaunchKernelGGL(place_tiles_kernel<uint32_t>, grid, dim3(256), 0, stream,
+                           static_cast<const uint32_t*>(gathered), static_cast<uint32_t*>(frame), row_u,
+                           tile_bytes / 4, H, N);
+    return hipGetLastError();
+}
+
 namespace {
 
 // Lanes per pixel (measured on one GPU's share of the N-GPU weak-scaling frame,

@@ -107,4 +107,11 @@ hipError_t build_tri_lbvh(const float4* d_tri, uint32_t n, const float lo[3], co
 
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 
+// Rank 0's placement after the gather (rt_place_tiles): frame row y comes from
+// tile y mod N, tile row y / N; `gathered` holds N tiles of tile_bytes back to
+// back.  One kernel on `stream` (device -> device), row_bytes and tile_bytes
+// multiples of 4.
+hipError_t launch_place_tiles(const void* gathered, void* frame, size_t row_bytes, size_t tile_bytes,
+                              uint32_t H, uint32_t N, hipStream_t stream);
+
 }  // namespace rt

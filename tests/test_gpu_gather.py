@@ -88,7 +88,9 @@ def test_place_tiles_n_ranks_equals_single_frame(H):
     W, spp = (1920 if H == 1080 else 40), 2  # W >= H: the reference's integer aspect
     s = Scene.cornell_box(W, H)
     with Renderer(s) as r:
-        stream = torch.cuda.current_stream()
+        # torch's current (null) stream, and a side stream at H = 17: the tile
+        # renders and the placement are ordered on the caller's stream
+        stream = torch.cuda.Stream() if H == 17 else torch.cuda.current_stream()
         for fp16, rgba8 in ((False, False), (True, False), (False, True)):
             ref = r.render(RenderParams(spp=spp, fp16=fp16, rgba8=rgba8))
             for world in (2, 3, 8, 16):
