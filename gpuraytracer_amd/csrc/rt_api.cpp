@@ -754,7 +754,10 @@ int rt_comm_init(rt_ctx* c, int32_t rank, int32_t world, const uint8_t id[RT_COM
 int rt_render_gather(rt_ctx* c, const rt_render_params* p, void* frame, void* hip_stream) {
     if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "ctx is null");
     DeviceGuard g(c->device);
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    // NULL is the HIP null stream (rt_render_async's convention): a caller on
+    // the default stream (torch's current stream is handle 0) gets its work
+    // ordered after everything it enqueued there
+    hipStream_t s = (hipStream_t)hip_stream;
     return render_gather_impl(c, p, frame, s);
 }
 
@@ -789,7 +792,10 @@ int rt_place_tiles(rt_ctx* c, const void* gathered_device, int32_t world, uint32
     if ((flags & RT_OUT_FP16) && (flags & RT_OUT_RGBA8))
         return fail(c, RT_ERR_INVALID_ARG, "RT_OUT_FP16 and RT_OUT_RGBA8 are exclusive");
     DeviceGuard g(c->device);
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    // NULL is the HIP null stream (rt_render_async's convention): a caller on
+    // the default stream (torch's current stream is handle 0) gets its work
+    // ordered after everything it enqueued there
+    hipStream_t s = (hipStream_t)hip_stream;
     return place_tiles_impl(c, gathered_device, (uint32_t)world, flags, frame, s);
 }
 

@@ -130,8 +130,8 @@ int rt_destroy(rt_ctx* ctx);
  * One process (or thread) per GPU, one context per GPU.  Rank k of N renders
  * the rows y = k, k+N, k+2N, ... with the global y (so the frame is
  * bit-identical to a single-GPU render) and the tiles are gathered to rank 0
- * by one ncclGather over xGMI, then placed at their rows by one strided copy
- * per rank.  The reference's draw (renderer.swift:117-146) has no multi-GPU
+ * by one ncclGather over xGMI, then placed at their rows by one kernel on rank
+ * 0 (rt_place_tiles).  The reference's draw (renderer.swift:117-146) has no multi-GPU
  * path; this extends it. */
 #define RT_COMM_ID_BYTES 128   /* ncclUniqueId */
 
@@ -149,7 +149,8 @@ int rt_comm_init(rt_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RT_C
  * row_count 0; the partition is y = rank (mod world)), then gather every tile into `frame` on rank 0 --
  * H*W pixels in the format of params->flags (rgba32F / rgba16F / RGBA8), host
  * memory (the call then blocks) or device memory with RT_OUT_DEVICE (enqueued
- * on `hip_stream`, NULL = the context's stream, no host sync).  `frame` is
+ * on `hip_stream`, a hipStream_t; NULL is the HIP null stream, as for
+ * rt_render_async; no host sync).  `frame` is
  * ignored on other ranks.  With RT_OUT_NONE (progressive batches into the
  * running sums) nothing is gathered.  RT_ERR_STATE without rt_comm_init,
  * RT_ERR_COMM when the gather fails. */
@@ -177,7 +178,7 @@ int rt_tile_layout(int32_t width, int32_t height, int32_t world, int32_t rank, u
  * holds `world` tiles of rt_tile_layout's tile_bytes back to back (device
  * memory); tile row j of rank k lands at frame row k + j*world.  `frame` is
  * H*W pixels in the format of flags, device memory with RT_OUT_DEVICE
- * (enqueued on hip_stream, NULL = the context's stream) or host memory (the
+ * (enqueued on hip_stream; NULL is the HIP null stream) or host memory (the
  * call blocks).  The same code rt_render_gather runs after its ncclGather. */
 int rt_place_tiles(rt_ctx* ctx, const void* gathered_device, int32_t world, uint32_t flags,
                    void* frame, void* hip_stream);
