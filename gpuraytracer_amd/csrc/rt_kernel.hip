@@ -131,6 +131,22 @@ template <int b, int B, int GEO, bool SPH, bool SMALL>
 struct BounceChain {
     __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv,
                                                PathState& s) {
+#ifdef RT_STATS
+        if constexpr (!SPH) {  // slots 16-31 are the sphere walks' in sphere scenes
+            // lane-slot accounting of the triangle kernels (tools/kernel_stats.py):
+            // shader-clock cycles of this bounce per wave, and the same weighted
+            // by the lanes whose path is still alive when it starts (16+b, 20+b)
+            const unsigned long long t0 = clock64();
+            const unsigned long long live = (unsigned long long)__popcll(__ballot(1));
+            const bool ok = bounce<b, B, GEO, SPH, SMALL>(P, sv, s);
+            const unsigned long long dt = clock64() - t0;
+            RT_STAT(16 + b, dt);
+            RT_STAT(20 + b, dt * live);
+            if (!ok) return;
+            BounceChain<b + 1, B, GEO, SPH, SMALL>::run(P, sv, s);
+            return;
+        }
+#endif
         if (!bounce<b, B, GEO, SPH, SMALL>(P, sv, s)) return;
         BounceChain<b + 1, B, GEO, SPH, SMALL>::run(P, sv, s);
     }
@@ -483,6 +499,9 @@ void path_trace_kernel(KParams P) {
     const float fW = (float)P.W, fH = (float)P.H;
     const uint32_t rounds = (P.spp + (L - 1)) / L;
     for (uint32_t r = 0; r < rounds; ++r) {                      // :34
+#ifdef RT_STATS
+        const unsigned long long t_round = clock64();  // slot 24: cycles of whole rounds
+#endif
         const uint32_t t = opaque_tid(), sub = t % L;
         // a lane past the last sample re-traces the last one (discarded below):
         // no divergent branch around the path
@@ -525,6 +544,12 @@ void path_trace_kernel(KParams P) {
                 lum_s[3 * slot + 2] = acc.z;
             }
         }
+#ifdef RT_STATS
+        if (!SPH) {
+            RT_STAT(24, clock64() - t_round);
+            RT_STAT(25, 1);
+        }
+#endif
     }
     const uint32_t t = opaque_tid();
     if (L > 1) {

@@ -15,8 +15,9 @@ from gpuraytracer_amd import RenderParams, Renderer, Scene, lib  # noqa: E402
 W, H, SPP = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 with Renderer(Scene.cornell_box(W, H)) as r:
     r.render(RenderParams(spp=SPP, bounces=3))
-    st = (ctypes.c_uint64 * 16)()
-    assert lib.rt_debug_stats(r._ctx, st, 16) == 0, lib.rt_last_error(r._ctx)
+    info = r.last_launch()
+    st = (ctypes.c_uint64 * 32)()
+    assert lib.rt_debug_stats(r._ctx, st, 32) == 0, lib.rt_last_error(r._ctx)
 names = ["camera", "bounce", "shadow"]
 samples = W * H * SPP
 out = {}
@@ -30,4 +31,27 @@ q, rounds, rl, ql = st[12:16]
 out["clusters"] = {"queries_per_wave": q, "rounds_per_query": rounds / max(q, 1),
                    "lanes_per_round": rl / max(rounds, 1), "lanes_per_query": ql / max(q, 1),
                    "candidate_tests_per_sample": rl / samples}
+# lane-slot accounting (shader-clock cycles per wave, slots 16-25): where a
+# wave's lanes sit idle because their path already ended (miss / light hit at
+# an earlier bounce) vs. the cycles of live lanes
+round_cyc, n_rounds = st[24], st[25]
+bounce = []
+idle_dead = 0.0
+for b in range(4):
+    cyc, cyc_live = st[16 + b], st[20 + b]
+    if not cyc:
+        continue
+    live = cyc_live / cyc / 64.0          # cycle-weighted live fraction at bounce entry
+    # lanes dead before bounce b idle for its whole duration
+    idle_dead += cyc * (1.0 - live)
+    bounce.append({"bounce": b, "cycles_share_of_rounds": cyc / max(round_cyc, 1),
+                   "live_lane_frac_at_entry": live})
+out["lane_slots"] = {
+    "kernel": info["kernel"], "lanes_per_pixel": info["lanes_per_pixel"],
+    "rounds_per_wave": n_rounds, "bounces": bounce,
+    # share of all round cycles x 64 lanes lost to lanes whose path had ended
+    "ended_path_idle_frac": idle_dead / max(round_cyc, 1),
+    "note": "remaining lane-slot loss (PMC lane util 1 - SQ_THREAD_CYCLES_VALU/"
+            "(64*SQ_ACTIVE_INST_VALU)) minus ended_path_idle_frac = divergence inside the "
+            "queries (candidate rounds) and shading branches"}
 print(json.dumps(out, indent=1))
