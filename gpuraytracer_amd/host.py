@@ -448,21 +448,23 @@ class Renderer:
     def place_tiles(self, gathered, world: int, out=None, fp16: bool = False, rgba8: bool = False,
                     stream=None):
         """rt_place_tiles: rank 0's placement step of rt_render_gather on a device
-        buffer ``gathered`` (``world`` padded tiles back to back).  Returns the
-        host frame, or fills the device tensor ``out`` on ``stream``."""
+        buffer ``gathered`` (``world`` padded tiles back to back), ordered on
+        ``stream`` (default: torch's current stream).  Returns the host frame
+        (blocking), or fills the device tensor ``out`` without a host sync."""
         gp = gathered if isinstance(gathered, int) else gathered.data_ptr()
         flags = _pixel_flags(fp16, rgba8)
-        if out is None:
-            dt = np.uint8 if rgba8 else np.uint16 if fp16 else np.float32
-            frame = np.empty((self.scene.height, self.scene.width, 4), dt)
-            _check(lib.rt_place_tiles(self._ctx, ctypes.c_void_p(gp), world, flags,
-                                      frame.ctypes.data_as(ctypes.c_void_p), None), self._ctx)
-            return frame
         if stream is None:
             import torch
             stream = torch.cuda.current_stream().cuda_stream
         elif hasattr(stream, "cuda_stream"):
             stream = stream.cuda_stream
+        if out is None:  # host frame: ordered on `stream` too, then the call blocks
+            dt = np.uint8 if rgba8 else np.uint16 if fp16 else np.float32
+            frame = np.empty((self.scene.height, self.scene.width, 4), dt)
+            _check(lib.rt_place_tiles(self._ctx, ctypes.c_void_p(gp), world, flags,
+                                      frame.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(stream)),
+                   self._ctx)
+            return frame
         ptr = out if isinstance(out, int) else out.data_ptr()
         _check(lib.rt_place_tiles(self._ctx, ctypes.c_void_p(gp), world, flags | RT_OUT_DEVICE,
                                   ctypes.c_void_p(ptr), ctypes.c_void_p(stream)), self._ctx)

@@ -98,7 +98,7 @@ def test_place_tiles_n_ranks_equals_single_frame(H):
                 dt = torch.uint8 if rgba8 else torch.int16 if fp16 else torch.float32
                 dev = torch.empty((H, W, 4), dtype=dt, device="cuda:0")
                 r.place_tiles(g, world, out=dev, fp16=fp16, rgba8=rgba8, stream=stream)
-                host = r.place_tiles(g, world, fp16=fp16, rgba8=rgba8)
+                host = r.place_tiles(g, world, fp16=fp16, rgba8=rgba8, stream=stream)
                 torch.cuda.synchronize()
                 d = dev.cpu().numpy().view(ref.dtype)
                 tag = f"H={H} N={world} fp16={fp16} rgba8={rgba8}"
