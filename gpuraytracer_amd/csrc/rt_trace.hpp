@@ -425,6 +425,12 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
 #ifdef RT_TIMING_NO_SPH_WALK  // timing-only experiment (share of the walks), NOT exact
     return;
 #endif
+#ifdef RT_TIMING_NO_SPH_ANY  // timing-only: share of the per-lane shadow walks, NOT exact
+    if (ANY) return;
+#endif
+#ifdef RT_TIMING_NO_SPH_CLOSEST  // timing-only: share of the per-lane closest walks, NOT exact
+    if (!ANY) return;
+#endif
     const float a = dot(d, d);
     const float a4 = 4.0f * a;
     const RayBox rb = ray_box(o, d);
