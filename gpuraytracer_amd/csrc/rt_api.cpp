@@ -862,11 +862,9 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
                      std::min(lds, lds_single) > rt::kMaxLdsBytes;
     info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
     {
-        const size_t sb = s.sph_lds.size() * 4 + ((s.sph_lds_id.size() * 2 + 3) & ~(size_t)3);
+        const size_t b = rt::sphere_lds_bytes(lds, s.sph_lds_entries, rt::kSphBlockThreads);
         info->sphere_bvh_lds_bytes =
-            (!s.sph_lds.empty() && lds <= rt::kMaxLdsBytes && lds + sb <= rt::kSphLdsMaxBytes)
-                ? (uint32_t)(lds + sb)
-                : 0u;
+            (!s.sph_lds.empty() && lds <= rt::kMaxLdsBytes && b <= rt::kSphLdsMaxBytes) ? (uint32_t)b : 0u;
     }
     // box clusters are staged after the pairs in triangle-only scenes
     const size_t lds_clu =

@@ -100,7 +100,9 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
     }
     if (FUSE && b + 1 < B) {
-        const FusedHit h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
+        const FusedHit h = GEO == kGeoPairClu
+                               ? fused_cluster_query(sv, p, L, dist - 1e-3f, d2)
+                               : fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
         if (!h.occluded) s.acc = s.acc + contrib;          // :79-89
         s.d = d2;
         s.o = p;                                           // :99-100
@@ -176,9 +178,12 @@ struct FusedChain<B, B, GEO, SMALL> {
 #ifndef RT_FUSED
 #define RT_FUSED 1
 #endif
+#ifndef RT_FUSED_CLU
+#define RT_FUSED_CLU 0  // 1: fused_cluster_query (measured 5 % slower on Cornell 1080p)
+#endif
 template <int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv, PathState& s) {
-    if (RT_FUSED && geo_pairs(GEO) && !SPH && B > 1) {
+    if (RT_FUSED && (geo_pairs(GEO) || (RT_FUSED_CLU && GEO == kGeoPairClu)) && !SPH && B > 1) {
         float t = 1000.0f;                                  // sampling.metal:155
         const int id = closest_hit<GEO, false, true, 0>(sv, s.o, s.d, 0.001f, &t);
         if (id >= 0) FusedChain<0, B, GEO, SMALL>::run(P, sv, s, id, t);
@@ -356,9 +361,6 @@ __host__ __device__ constexpr bool halton_tables_on(int geo, bool small, uint32_
 // order n — the same sequence of fp32 additions as one lane per pixel.
 // Workgroup size: 1024 threads (4x4 waves) when the sphere BVH is staged in
 // LDS, so one ~72 KB copy serves 16 waves; 256 (2x2 waves) otherwise.
-#ifndef RT_SPH_BLOCK
-#define RT_SPH_BLOCK 1024  // threads per workgroup of the LDS-sphere-BVH kernel (768: 4x3 waves)
-#endif
 constexpr uint32_t block_threads(int geo) { return geo == kGeoSphLds ? RT_SPH_BLOCK : kBlockThreads; }
 constexpr uint32_t waves_per_row(int geo) { return geo == kGeoSphLds ? 4u : 2u; }
 constexpr uint32_t waves_per_col(int geo) { return block_threads(geo) / 64u / waves_per_row(geo); }
@@ -384,16 +386,24 @@ void path_trace_kernel(KParams P) {
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
-        if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) + entry ids after the pairs
+        if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) after the pairs
             const uint32_t ne = 2u * P.nE;
             const uint4* es = reinterpret_cast<const uint4*>(P.sph_lds);
             uint4* ed = reinterpret_cast<uint4*>(lds + ng4);
             for (uint32_t k = threadIdx.x; k < ne; k += NT) ed[k] = es[k];
+            sv.sent = ed;
+#if RT_SPH_SPLIT
+            // then one scratch per wave for the split walks; the entry ids
+            // (read only for a root that wins) stay in global memory
+            sv.wscr = reinterpret_cast<uint8_t*>(lds + ng4 + ne) +
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * kWaveScratchBytes;
+            sv.sid = P.sph_lds_id;
+#else
             const uint32_t* is = reinterpret_cast<const uint32_t*>(P.sph_lds_id);
             uint32_t* id = reinterpret_cast<uint32_t*>(lds + ng4 + ne);
             for (uint32_t k = threadIdx.x; k < (ne + 1) / 2; k += NT) id[k] = is[k];
-            sv.sent = ed;
             sv.sid = reinterpret_cast<const uint16_t*>(id);
+#endif
         }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
@@ -838,7 +848,7 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     size_t lds_total = lds_bytes;
     // sphere BVH in LDS (1024-thread workgroups, two per CU) when it fits
     if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto) {
-        const size_t b = lds_bytes + 2u * P.nE * 16u + ((2u * P.nE * 2u + 3u) & ~3u);
+        const size_t b = sphere_lds_bytes(lds_bytes, P.nE, RT_SPH_BLOCK);
         if (b <= kSphLdsMaxBytes) {
             geo = kGeoSphLds;
             lds_total = b;

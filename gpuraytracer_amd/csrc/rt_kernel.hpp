@@ -19,6 +19,26 @@ constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padde
 // CU share 160 KB with their static per-pixel sums (3 KB at 4 lanes per pixel)
 // and per-lane seeds (4 KB): 80 KB - 7 KB each
 constexpr size_t kSphLdsMaxBytes = 73 * 1024;
+// Per-lane sphere walks split across the lanes of a wave (rt_trace.hpp
+// sphere_walk_lds): each wave of the LDS-sphere kernel owns a 576-B LDS
+// scratch (64 B rank map + 64 u64 result slots), and the sphere ids of the
+// compact BVH entries are then read from global memory instead of LDS.
+#ifndef RT_SPH_SPLIT
+#define RT_SPH_SPLIT 0  // measured: wave steps -40 %, no faster; opt-in
+#endif
+constexpr uint32_t kWaveScratchBytes = 576;
+// dynamic LDS of the LDS-sphere kernel: pair records, both layouts of the
+// compact BVH, then the wave scratch (RT_SPH_SPLIT) or the entry ids
+inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t block_threads) {
+    const size_t ent = 2u * (size_t)n_entries * 16u;
+    return pair_bytes + ent +
+           (RT_SPH_SPLIT ? (size_t)(block_threads / 64u) * kWaveScratchBytes
+                         : ((2u * (size_t)n_entries * 2u + 3u) & ~(size_t)3u));
+}
+#ifndef RT_SPH_BLOCK
+#define RT_SPH_BLOCK 1024  // threads per workgroup of the LDS-sphere-BVH kernel (768: 4x3 waves)
+#endif
+constexpr uint32_t kSphBlockThreads = RT_SPH_BLOCK;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).

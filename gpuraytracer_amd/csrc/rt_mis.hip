@@ -176,12 +176,32 @@ __device__ __forceinline__ int mis_closest(const SceneView& sv, f3 o, f3 d, floa
     return closest_hit<GEO, false, true, 0>(sv, o, d, 0.001f, t);
 }
 
+// The primary hit x of the current camera ray: point and ray direction in a
+// per-lane LDS stash (MisHitStash, written once per camera ray), re-read where
+// they are used -- through an opaque lane index, so the reads are not hoisted
+// back into registers across the MIS sample loops (the queries nested in them
+// are where the register pressure peaks).
+__device__ __forceinline__ uint32_t opaque_lane_slot() { return opaque_u32(threadIdx.x); }
+__device__ __forceinline__ MisHit load_x(const SceneView& sv, uint32_t id) {
+    const uint32_t k = opaque_lane_slot();
+    const float* st = sv.xstash;
+    MisHit x;
+    x.p = f3{st[k], st[kBlockThreads + k], st[2 * kBlockThreads + k]};
+    x.din = f3{st[3 * kBlockThreads + k], st[4 * kBlockThreads + k], st[5 * kBlockThreads + k]};
+    x.id = id;
+    return x;
+}
+
 // calculateDirectLightSamplingContribution (:519-541).  POWER: MIS-weighted
-// (first hit) or plain (at the secondary hit, samplesPerStrategy = 1).
+// (first hit) or plain (at the secondary hit, samplesPerStrategy = 1).  The
+// contribution is formed BEFORE the visibility query (the same operations:
+// nothing in it depends on the query), so only it and the query's ray are live
+// during the query.
 template <int GEO, bool POWER>
 __device__ __forceinline__ f3 direct_light(const MisParams& P, const SceneView& sv, const MisHit& x,
                                            float ux, float uy, float nS) {
-    const f3 origin = x.p + hit_n(sv, x) * 1e-4f;
+    const f3 n = hit_n(sv, x);
+    const f3 origin = x.p + n * 1e-4f;
     // directSquareLightRay (:291-313)
     const float sx = (ux - 0.5f) * P.l_width;
     const float sy = (uy - 0.5f) * P.l_depth;
@@ -191,37 +211,42 @@ __device__ __forceinline__ f3 direct_light(const MisParams& P, const SceneView& 
     const f3 tl = sp - origin;
     const float dist = length(tl);
     const f3 L{tl.x / dist, tl.y / dist, tl.z / dist};
+    f3 contrib;
+    {
+        const float dl_pdf = light_pdf(P, x.p, L);
+        const MisMat m = hit_m(sv, x);
+        const f3 c = brdf(x.din, n, m, L);
+        const f3 Le{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
+        if (POWER) {
+            const float cos_pdf = cosine_pdf(n, L);
+            const float v_pdf = vndf_pdf(-x.din, n, L, m.roughness);
+            const float w = power_h(dl_pdf, cos_pdf, v_pdf, nS);
+            const f3 a = (c * w) * Le;
+            contrib = f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
+        } else {
+            const f3 a = c * Le;
+            contrib = f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
+        }
+    }
     float t;
     const int id = mis_closest<GEO>(sv, origin, L, dist, &t);
     if (id < 0 || sv.shade[3 * id].w == 0.0f) return f3{0.0f, 0.0f, 0.0f};  // not HitLight
-    const float dl_pdf = light_pdf(P, x.p, L);
-    const f3 n = hit_n(sv, x);
-    const MisMat m = hit_m(sv, x);
-    const f3 c = brdf(x.din, n, m, L);
-    const f3 Le{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
-    if (POWER) {
-        const float cos_pdf = cosine_pdf(n, L);
-        const float v_pdf = vndf_pdf(-x.din, n, L, m.roughness);
-        const float w = power_h(dl_pdf, cos_pdf, v_pdf, nS);
-        const f3 a = (c * w) * Le;
-        return f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
-    }
-    const f3 a = c * Le;
-    return f3{a.x / dl_pdf, a.y / dl_pdf, a.z / dl_pdf};
+    return contrib;
 }
 
 // Continuation of a cosine or VNDF sample (:576-590, :608-622): the sampled
 // ray's closest hit either sees the light (MIS-weighted emission) or a
-// surface (next-event estimate there, unweighted).
+// surface (next-event estimate there, unweighted).  brdf(x, dir) does not
+// depend on the hit: it is formed before the query.
 template <int GEO>
 __device__ __forceinline__ f3 continue_sample(const MisParams& P, const SceneView& sv,
                                               const MisHit& x, f3 origin, f3 dir, float pdf,
                                               float w, float u2x, float u2y) {
+    const f3 c = brdf(x.din, hit_n(sv, x), hit_m(sv, x), dir);
     float t;
     const int id = mis_closest<GEO>(sv, origin, dir, 1000.0f, &t);
     if (id < 0) return f3{0.0f, 0.0f, 0.0f};
     const float4 r0 = sv.shade[3 * id];
-    const f3 c = brdf(x.din, hit_n(sv, x), hit_m(sv, x), dir);
     if (r0.w != 0.0f) {  // HitLight
         const f3 a = (c * w) * f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
         return f3{a.x / pdf, a.y / pdf, a.z / pdf};
@@ -234,23 +259,26 @@ __device__ __forceinline__ f3 continue_sample(const MisParams& P, const SceneVie
     return q * direct_light<GEO, false>(P, sv, y, u2x, u2y, 1.0f);
 }
 
-// recursiveMultiImportanceSampling (:543-625)
+// recursiveMultiImportanceSampling (:543-625).  x (point, direction) is re-read
+// from the lane's LDS stash per sample and the tangent frame of onb() (a
+// function of the normal only) is recomputed per sample: the same values, held
+// in no register across the nested queries.
 template <int GEO>
-__device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView& sv,
-                                            const MisHit& x) {
+__device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView& sv, uint32_t xid) {
     const uint32_t S = P.S;
     const float nS = (float)S;
     const float4* __restrict__ tab = P.u_tab;
     f3 dl{0.0f, 0.0f, 0.0f}, cs{0.0f, 0.0f, 0.0f}, vn{0.0f, 0.0f, 0.0f};
     for (uint32_t i = 0; i < S; ++i) {  // light sampling (:553-560)
         const float4 u = tab[3 * i];
-        dl = dl + direct_light<GEO, true>(P, sv, x, u.x, u.y, nS);
+        dl = dl + direct_light<GEO, true>(P, sv, load_x(sv, xid), u.x, u.y, nS);
     }
-    f3 t, b;
-    onb(hit_n(sv, x), &t, &b);
     for (uint32_t i = 0; i < S; ++i) {  // cosine-hemisphere sampling (:562-591)
         const float4 u = tab[3 * i + 1];
+        const MisHit x = load_x(sv, xid);
         const f3 n = hit_n(sv, x);
+        f3 t, b;
+        onb(n, &t, &b);
         const f3 origin = x.p + n * 1e-4f;
         const f3 V = -x.din;
         const f3 dir = cosine_dir(n, t, b, u.x, u.y);
@@ -263,7 +291,10 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
     const f3 dc = dl + cs;  // (directLight + cosine) + vndf (:624), same order
     for (uint32_t i = 0; i < S; ++i) {  // VNDF sampling (:593-623)
         const float4 u = tab[3 * i + 2];
+        const MisHit x = load_x(sv, xid);
         const f3 n = hit_n(sv, x);
+        f3 t, b;
+        onb(n, &t, &b);
         const f3 origin = x.p + n * 1e-4f;
         const f3 V = -x.din;
         const float rough = hit_m(sv, x).roughness;
@@ -317,6 +348,7 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         for (uint32_t k = threadIdx.x; k < 3u * sv.nT; k += kBlockThreads)
             lds[ng4 + nc4 + k] = P.mis_shade[k];
         sv.shade = lds + ng4 + nc4;
+        sv.xstash = reinterpret_cast<float*>(lds + ng4 + nc4 + 3u * sv.nT);
         __syncthreads();
         sv.tri = lds;
         sv.pair = lds;
@@ -327,7 +359,10 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
     }
-    if (GEO == kGeoTriBvh || GEO == kGeoTriGlobal) sv.shade = P.mis_shade;
+    if (GEO == kGeoTriBvh || GEO == kGeoTriGlobal) {
+        sv.shade = P.mis_shade;
+        sv.xstash = reinterpret_cast<float*>(lds);
+    }
 
     // pixel of a lane; recomputed from an opaque threadIdx where it is used
     // (as in rt_kernel.hip), not held across the camera-ray loop
@@ -368,11 +403,18 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
             acc = acc + f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
             continue;
         }
-        MisHit h;
-        h.p = cpos + d * t;
-        h.din = d;
-        h.id = (uint32_t)id;
-        acc = acc + mis_shade_hit<GEO>(P, sv, h);           // :674-676
+        {  // the primary hit x into this lane's stash
+            const f3 hp = cpos + d * t;
+            float* st = sv.xstash;
+            const uint32_t k = threadIdx.x;
+            st[k] = hp.x;
+            st[kBlockThreads + k] = hp.y;
+            st[2 * kBlockThreads + k] = hp.z;
+            st[3 * kBlockThreads + k] = d.x;
+            st[4 * kBlockThreads + k] = d.y;
+            st[5 * kBlockThreads + k] = d.z;
+        }
+        acc = acc + mis_shade_hit<GEO>(P, sv, (uint32_t)id);  // :674-676
     }
     const float nc = (float)P.camera_rays;
     uint32_t x, j;
@@ -394,6 +436,8 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     }
 }
 
+constexpr size_t kMisStashBytes = 6u * kBlockThreads * sizeof(float);  // per-lane primary hit (p, din)
+
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + shading records
     return (size_t)((n_pairs ? kPairF4 * n_pairs : 3u * n_tri) + 3u * n_tri) * sizeof(float4);
 }
@@ -403,18 +447,19 @@ hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
     const bool pairs = mem != SceneMem::kLdsSingle && P.nP > 0;
     const size_t lds = mis_lds_bytes(P.nT, pairs ? P.nP : 0u);
     const bool lds_ok = mem != SceneMem::kSmem && lds <= kMaxLdsBytes;
+    const size_t X = kMisStashBytes;
     if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) {
-        hipLaunchKernelGGL(mis_kernel<kGeoTriBvh>, grid, dim3(kBlockThreads), 0, stream, P);
-    } else if (lds_ok) {
+        hipLaunchKernelGGL(mis_kernel<kGeoTriBvh>, grid, dim3(kBlockThreads), X, stream, P);
+    } else if (lds_ok && lds + X <= kMaxLdsBytes) {
         const size_t lds_clu = lds + kCluF4 * P.nC * sizeof(float4);
-        if (pairs && P.nC > 0 && mem == SceneMem::kAuto && lds_clu <= kMaxLdsBytes)
-            hipLaunchKernelGGL(mis_kernel<kGeoPairClu>, grid, dim3(kBlockThreads), lds_clu, stream, P);
+        if (pairs && P.nC > 0 && mem == SceneMem::kAuto && lds_clu + X <= kMaxLdsBytes)
+            hipLaunchKernelGGL(mis_kernel<kGeoPairClu>, grid, dim3(kBlockThreads), lds_clu + X, stream, P);
         else if (pairs)
-            hipLaunchKernelGGL(mis_kernel<kGeoPairLds>, grid, dim3(kBlockThreads), lds, stream, P);
+            hipLaunchKernelGGL(mis_kernel<kGeoPairLds>, grid, dim3(kBlockThreads), lds + X, stream, P);
         else
-            hipLaunchKernelGGL(mis_kernel<kGeoTriLds>, grid, dim3(kBlockThreads), lds, stream, P);
+            hipLaunchKernelGGL(mis_kernel<kGeoTriLds>, grid, dim3(kBlockThreads), lds + X, stream, P);
     } else {
-        hipLaunchKernelGGL(mis_kernel<kGeoTriGlobal>, grid, dim3(kBlockThreads), 0, stream, P);
+        hipLaunchKernelGGL(mis_kernel<kGeoTriGlobal>, grid, dim3(kBlockThreads), X, stream, P);
     }
     return hipGetLastError();
 }

@@ -435,6 +435,9 @@ static void build_sphere_lds(CompiledScene* out) {
     std::vector<uint32_t> ent;
     std::vector<uint16_t> ids;
     for (int oct : {0, 7}) {
+        // escapes are entry indices of the concatenated layouts (layout 1
+        // starts at ne), so a walk's position alone names its layout
+        const uint32_t lay_base = oct == 0 ? 0u : ne;
         const BvhNode* L = out->sph_nodes.data() + (size_t)oct * nn;
         uint32_t k = 0;  // running entry index of this layout
         std::vector<uint32_t> lpos(nn + 1);
@@ -454,7 +457,7 @@ static void build_sphere_lds(CompiledScene* out) {
                 }
                 if (n.escape > nn) return;
                 const uint32_t w[4] = {h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,
-                                       h[4] | (uint32_t)h[5] << 16, lpos[n.escape] | 0x80000000u};
+                                       h[4] | (uint32_t)h[5] << 16, (lay_base + lpos[n.escape]) | 0x80000000u};
                 ent.insert(ent.end(), w, w + 4);
                 ids.push_back(0);
             } else {

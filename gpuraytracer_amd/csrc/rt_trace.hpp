@@ -162,8 +162,10 @@ struct SceneView {
     uint32_t pair_free;       // pairs in no cluster: tested by every lane
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
     const uint4* sent;        // compact sphere BVH entries in LDS (kGeoSphLds), 2 layouts
-    const uint16_t* sid;      // sphere id of each entry (leaves)
+    const uint16_t* sid;      // sphere id of each entry (leaves): LDS, or global with RT_SPH_SPLIT
+    uint8_t* wscr;            // this wave's LDS scratch for split walks (kWaveScratchBytes)
     const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
+    float* xstash;            // MIS: per-lane primary hit (p, din), SoA in LDS (rt_mis.hip)
 };
 
 // min / max of the culling tests, issued directly.  fminf/fmaxf lower to
@@ -360,6 +362,9 @@ __device__ __forceinline__ float h2f(uint32_t b16) {
 }
 
 __device__ __forceinline__ uint32_t lds_layout(f3 d) {
+#ifdef RT_SPH_ONE_LAYOUT  // experiment: every ray walks layout (+,+,+) (speed only)
+    return 0u;
+#endif
     return __builtin_popcount(octant(d)) >= 2 ? 1u : 0u;
 }
 
@@ -377,11 +382,12 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
     const uint32_t lay = PACKET ? wave_uniform(lds_layout(d)) : lds_layout(d);
-    ent += lay * nN;
-    ids += lay * nN;
-    uint32_t idx = 0;
+    // entry indices (and escapes) run over both layouts: layout `lay` is
+    // [lay * nN, (lay + 1) * nN)
+    uint32_t idx = lay * nN;
+    const uint32_t end = idx + nN;
     if (PACKET) RT_STAT(23, 1);
-    while (idx < nN) {
+    while (idx < end) {
         if (PACKET) RT_STAT(31, 1);
         const uint4 e = ent[idx];
         uint32_t next = idx + 1;
@@ -417,10 +423,36 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
 // visited in the same order and every value is sph_test's, ranked by (t, id):
 // the same result.  ANY: *id becomes >= 0 on the first accepted hit (and that
 // lane stops).
-template <bool ANY>
+//
+// SPLIT: a wave no longer waits with idle lanes for its
+// longest walk.  A walk is a range [idx, end) of the depth-first entry order
+// (stackless: walking from any entry m to end visits everything of the
+// subtrees from m on that the full walk would, plus possibly more).  When at
+// least RT_SPH_SPLIT_MIN lanes of the wave have finished, every walking lane
+// offers the rest of its range after the current subtree ([escape, end); or
+// after the first child when the subtree is all that is left), and the k-th
+// idle lane takes the k-th offer: it pulls the ray, the running (best, id) and
+// the range through cross-lane reads (ds_bpermute), the giver keeps
+// [idx, split).  Takers may be split again.  At the end every lane delivers
+// its (t, id) to the walk's original lane with an LDS atomic min of the key
+// (t bits << 32 | id + 1) -- exactly the (t, id) ranking, since every t here
+// is positive -- and every lane reads back its own query's result.  Extra
+// entries visited by a split walk can only add candidates that are real hits
+// in (tmin, tmax), so the minimum is the brute-force one.
+#ifndef RT_SPH_SPLIT_CLOSEST_ONLY
+#define RT_SPH_SPLIT_CLOSEST_ONLY 0  // 1: shadow (any-hit) walks are not split
+#endif
+#ifndef RT_SPH_SPLIT_MIN
+#define RT_SPH_SPLIT_MIN 16  // idle lanes of a wave that trigger a split round
+#endif
+__device__ __forceinline__ unsigned long long walk_key(float best, int id) {
+    return ((unsigned long long)__float_as_uint(best) << 32) | (uint32_t)(id + 1);
+}
+
+template <bool ANY, bool SPLIT>
 __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t* ids, uint32_t nN,
                                                 uint32_t nT, f3 o, f3 d, float tmin, float& best,
-                                                int& id) {
+                                                int& id, uint8_t* wscr) {
     constexpr uint32_t kNone = 0xFFFFFFFFu;
 #ifdef RT_TIMING_NO_SPH_WALK  // timing-only experiment (share of the walks), NOT exact
     return;
@@ -431,21 +463,34 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
 #ifdef RT_TIMING_NO_SPH_CLOSEST  // timing-only: share of the per-lane closest walks, NOT exact
     if (!ANY) return;
 #endif
-    const float a = dot(d, d);
-    const float a4 = 4.0f * a;
-    const RayBox rb = ray_box(o, d);
-    const uint32_t lay = lds_layout(d);
-    ent += lay * nN;
-    ids += lay * nN;
-    uint32_t idx = (ANY && id >= 0) ? nN : 0u;  // next entry of this lane's walk (nN: done)
+    float a = dot(d, d);
+    RayBox rb = ray_box(o, d);
+    // entry range of this lane's walk over the concatenated layouts
+    uint32_t idx = lds_layout(d) * nN;
+    uint32_t end = idx + nN;
+    if (ANY && id >= 0) idx = end;
     uint32_t leaf = kNone;                      // the parked leaf
     float pb = 0.0f, pdisc = 0.0f;              // its b and discriminant
+    [[maybe_unused]] const uint32_t lane = __lane_id();
+    [[maybe_unused]] uint32_t owner = lane;     // lane whose query this walk serves
+    [[maybe_unused]] bool split_any = false;    // wave-uniform
+    // the wave scratch as LDS pointers (a generic pointer would become flat
+    // accesses): rank map [64] bytes, then 64 result keys
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+    lds_u8* rank_map = (lds_u8*)wscr;
+    lds_u64* res = (lds_u64*)(wscr + 64);
+    [[maybe_unused]] const int n_exec = __popcll(__builtin_amdgcn_ballot_w64(true));
+    // split when RT_SPH_SPLIT_MIN more lanes are idle than the last round
+    // left without work (no offer for them): a wave whose remaining walks
+    // cannot be split any more does not retry every step
+    [[maybe_unused]] int split_at = RT_SPH_SPLIT_MIN;  // wave-uniform
     [[maybe_unused]] constexpr int ST = ANY ? 24 : 16;
     RT_STAT(ST, 1);
     RT_STAT(ST + 1, __popcll(__ballot(1)));
     for (;;) {
-        for (;;) {  // cheap steps until the lane parks a leaf or leaves the tree
-            const bool adv = idx < nN && leaf == kNone;
+        for (;;) {  // cheap steps until the lane parks a leaf or leaves its range
+            const bool adv = idx < end && leaf == kNone;
             if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
             RT_STAT(ST + 2, 1);
             RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(adv)));
@@ -458,7 +503,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
                                          __uint_as_float(e.z)};
                     const float bq = 2.0f * dot(oc, d);
                     const float cc = dot(oc, oc) - __uint_as_float(e.w);
-                    const float disc = bq * bq - a4 * cc;
+                    const float disc = bq * bq - (4.0f * a) * cc;
                     if (disc > 0.0f) {
                         leaf = idx;
                         pb = bq;
@@ -468,8 +513,78 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
                 }
             }
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
-            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < nN || leaf != kNone));
+            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
             if (2 * parked >= live) break;
+            if constexpr (SPLIT) {
+                if (n_exec - live >= split_at) {  // lanes with nothing to walk
+                    RT_STAT(ST + 4, 1);
+                    const bool idle = idx >= end && leaf == kNone;
+                    const unsigned long long idle_m = __builtin_amdgcn_ballot_w64(idle);
+                    if (!split_any) {  // first split of this walk: empty result slots
+                        res[lane] = ANY ? 0ull : ~0ull;
+                        split_any = true;
+                    }
+                    // offer: the part of the range after the current subtree
+                    uint32_t m = end;
+                    if (idx < end && leaf == kNone) {
+                        const uint4 e = ent[idx];
+                        if (e.w & 0x80000000u) {
+                            const uint32_t esc = e.w & 0x7FFFFFFFu;
+                            if (esc < end) {
+                                m = esc;
+                            } else {  // the subtree is all that is left: offer its 2nd child on
+                                const uint32_t w1 = ent[idx + 1].w;
+                                m = (w1 & 0x80000000u) ? (w1 & 0x7FFFFFFFu) : idx + 2;
+                            }
+                        } else {
+                            m = idx + 1;
+                        }
+                    }
+                    const bool can = m < end;
+                    const unsigned long long can_m = __builtin_amdgcn_ballot_w64(can);
+                    const uint32_t n = (uint32_t)min(__popcll(can_m), __popcll(idle_m));
+                    const uint32_t rc = __builtin_amdgcn_mbcnt_hi((uint32_t)(can_m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)can_m, 0u));
+                    const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle_m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle_m, 0u));
+                    const bool giver = can && rc < n;
+                    const bool taker = idle && ri < n;
+                    split_at = (__popcll(idle_m) - (int)n) + RT_SPH_SPLIT_MIN;
+                    if (giver) rank_map[rc] = (uint8_t)lane;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const int src = taker ? (int)rank_map[ri] : (int)lane;
+                    // the taker's finished query result goes to its query's lane
+                    if (taker) {
+                        if (ANY)
+                            __hip_atomic_fetch_max(&res[owner], id >= 0 ? 1ull : 0ull, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        else
+                            __hip_atomic_fetch_min(&res[owner], walk_key(best, id), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    }
+                    // the giver's ray, running (best, id), split point, range end
+                    // and query lane (two 16-bit fields per word where they fit)
+                    const f3 o2{__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src)};
+                    const f3 d2{__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src)};
+                    const float best2 = __shfl(best, src);
+                    const uint32_t range2 = (uint32_t)__shfl((int)(m | (end << 16)), src);
+                    const uint32_t who2 = (uint32_t)__shfl((int)(owner | ((uint32_t)(id + 1) << 8)), src);
+                    if (taker) {
+                        o = o2;
+                        d = d2;
+                        a = dot(d, d);
+                        rb = ray_box(o, d);
+                        best = best2;
+                        id = (int)(who2 >> 8) - 1;
+                        idx = range2 & 0xFFFFu;
+                        end = range2 >> 16;
+                        owner = who2 & 0xFFu;
+                    }
+                    if (giver) end = m;
+                }
+            }
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
         RT_STAT(ST + 5, 1);
@@ -482,7 +597,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             if (ANY) {
                 if (t > tmin && t < best) {
                     id = 0;
-                    idx = nN;
+                    idx = end;
                 }
             } else if (t > tmin && t < 3.0e38f && t <= best) {
                 const int s = (int)(nT + ids[leaf]);
@@ -494,6 +609,28 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             leaf = kNone;
         }
     }
+    if constexpr (SPLIT) {
+        if (split_any) {  // every walk's (t, id) to its query's lane; read back this lane's own
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (ANY)
+                __hip_atomic_fetch_max(&res[owner], id >= 0 ? 1ull : 0ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
+            else
+                __hip_atomic_fetch_min(&res[owner], walk_key(best, id), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const unsigned long long k = res[lane];
+            if (ANY) {
+                id = k ? 0 : -1;
+            } else {
+                best = __uint_as_float((uint32_t)(k >> 32));
+                id = (int)(uint32_t)k - 1;
+            }
+        }
+    }
 }
 
 template <bool PACKET>
@@ -502,10 +639,10 @@ __device__ __forceinline__ bool sphere_any_lds(const uint4* ent, uint32_t nN, f3
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
     const uint32_t lay = PACKET ? wave_uniform(lds_layout(d)) : lds_layout(d);
-    ent += lay * nN;
     bool found = false;
-    uint32_t idx = 0;
-    while (idx < nN) {
+    uint32_t idx = lay * nN;
+    const uint32_t end = idx + nN;
+    while (idx < end) {
         const uint4 e = ent[idx];
         uint32_t next = idx + 1;
         if (e.w & 0x80000000u) {
@@ -863,7 +1000,8 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
     if (SPH && GEO == kGeoSphLds && ((CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3))
         sphere_closest_lds<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
     else if (SPH && GEO == kGeoSphLds)
-        sphere_walk_lds<false>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
+        sphere_walk_lds<false, RT_SPH_SPLIT != 0>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id,
+                                                  sv.wscr);
     else if (SPH)
         sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
     *t_io = best;
@@ -922,7 +1060,8 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
     if (SPH && GEO == kGeoSphLds) {
         float tm = tmax;
         int id = -1;
-        sphere_walk_lds<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id);
+        sphere_walk_lds<true, RT_SPH_SPLIT != 0 && !RT_SPH_SPLIT_CLOSEST_ONLY>(
+            sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id, sv.wscr);
         return id >= 0;
     }
     if (SPH) return sphere_any<PACKET>(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
@@ -988,6 +1127,76 @@ __device__ __forceinline__ FusedHit fused_shadow_closest(const SceneView& sv, f3
             }
         }
     }
+    return h;
+}
+
+// Fused shadow any-hit of bounce b and closest hit of bounce b+1 over the box
+// clusters (kGeoPairClu; the cluster twin of fused_shadow_closest): both rays
+// start at p, so after both candidate masks are formed each lane tests ONE
+// candidate pair per round -- a shadow candidate while its shadow ray is not yet
+// occluded, else a closest candidate -- instead of running the shadow rounds
+// and then the closest rounds each to the wave's longest list.  Every test is
+// pair_test_rank's (same arithmetic, same (t, id) ranking, candidates visited
+// out of id order as there), so each lane's two results are exactly those of
+// cluster_query<true> and cluster_query<false>.
+__device__ __forceinline__ FusedHit fused_cluster_query(const SceneView& sv, f3 p, f3 L, float smax,
+                                                        f3 d2) {
+    FusedHit h{false, -1, 1000.0f};  // max_distance (sampling.metal:155)
+    float tm = smax;
+    int sid = -1;
+    for (uint32_t free = sv.pair_free; free != 0u; free &= free - 1u) {
+        const uint32_t k = (uint32_t)__builtin_ctz(free);
+        pair_test_rank<true>(sv.pair + kPairF4 * k, k, p, L, 0.0f, &tm, &sid);
+        pair_test_rank<false>(sv.pair + kPairF4 * k, k, p, d2, 0.001f, &h.t, &h.id);
+    }
+    uint32_t cs = sid >= 0 ? 0u : cluster_candidates<true>(sv, p, L, 0.0f, smax);
+    uint32_t cc = cluster_candidates<false>(sv, p, d2, 0.001f, h.t);
+    while ((cs | cc) != 0u) {
+        const bool shadow = cs != 0u;
+        const uint32_t k = (uint32_t)__builtin_ctz(shadow ? cs : cc);
+        if (shadow)
+            cs &= cs - 1u;
+        else
+            cc &= cc - 1u;
+        // pair_test_rank with the mode chosen per lane
+        const f3 dir = shadow ? L : d2;
+        const float tmin = shadow ? 0.0f : 0.001f;
+        const float4* rr = sv.pair + kPairF4 * k;
+        const float4 r0 = rr[0], r1 = rr[1], r2 = rr[2], r3 = rr[3], r4 = rr[4];
+        const PairDots q = pair_dots(r0, r1, r2, r3, r4, p, dir);
+        const bool pa = bary_ok(q.denA, q.a1, q.a2);
+        const bool pb = bary_ok(q.denB, q.b1, q.b2);
+        if (pa || pb) {
+            const float best = shadow ? smax : h.t;
+            const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+            const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
+            const int ia = (int)(pa ? 2 * k : 2 * k + 1);
+            bool hit = t > tmin && (t < best || (!shadow && t == best && ia < h.id));
+            float tb = t;
+            int ib = ia;
+            if (pa && pb) {
+                const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
+                const int i2 = (int)(2 * k + 1);
+                const float best2 = hit ? tb : best;
+                const int id2 = hit ? ib : h.id;
+                if (t2 > tmin && (t2 < best2 || (!shadow && t2 == best2 && i2 < id2))) {
+                    hit = true;
+                    tb = t2;
+                    ib = i2;
+                }
+            }
+            if (hit) {
+                if (shadow) {
+                    h.occluded = true;
+                    cs = 0u;  // any hit ends the shadow query (cluster_query<true>)
+                } else {
+                    h.t = tb;
+                    h.id = ib;
+                }
+            }
+        }
+    }
+    h.occluded = h.occluded || sid >= 0;
     return h;
 }
 

@@ -28,6 +28,7 @@ for name, b in (("closest", 16), ("any", 24)):
         "step_lane_util": step_lanes / max(64 * steps, 1),
         "lane_steps_per_lane_walk": step_lanes / max(lanes, 1),
         "root_rounds_per_walk": rounds / max(walks, 1),
+        "split_rounds_per_walk": leaf_lanes / max(walks, 1),  # slot +4: split rounds (RT_SPH_SPLIT)
         "parked_per_round": parked / max(rounds, 1),
         "roots_per_lane_walk": parked / max(lanes, 1),
     }
