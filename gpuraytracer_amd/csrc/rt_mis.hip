@@ -177,7 +177,7 @@ __device__ __forceinline__ int mis_closest(const SceneView& sv, f3 o, f3 d, floa
 }
 
 // The primary hit x of the current camera ray: point and ray direction in a
-// per-lane LDS stash (MisHitStash, written once per camera ray), re-read where
+// per-lane LDS stash (slots 0-5, written once per camera ray), re-read where
 // they are used -- through an opaque lane index, so the reads are not hoisted
 // back into registers across the MIS sample loops (the queries nested in them
 // are where the register pressure peaks).
@@ -273,6 +273,13 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float4 u = tab[3 * i];
         dl = dl + direct_light<GEO, true>(P, sv, load_x(sv, xid), u.x, u.y, nS);
     }
+    {  // dl waits in the stash through the cosine loop
+        float* st = sv.xstash;
+        const uint32_t k = threadIdx.x;
+        st[9 * kBlockThreads + k] = dl.x;
+        st[10 * kBlockThreads + k] = dl.y;
+        st[11 * kBlockThreads + k] = dl.z;
+    }
     for (uint32_t i = 0; i < S; ++i) {  // cosine-hemisphere sampling (:562-591)
         const float4 u = tab[3 * i + 1];
         const MisHit x = load_x(sv, xid);
@@ -288,7 +295,17 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float w = power_h(cos_pdf, dl_pdf, v_pdf, nS);
         cs = cs + continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w);
     }
-    const f3 dc = dl + cs;  // (directLight + cosine) + vndf (:624), same order
+    {  // (directLight + cosine) + vndf (:624), same order; dc waits in the stash
+        const uint32_t k0 = opaque_lane_slot();
+        const f3 dl2{sv.xstash[9 * kBlockThreads + k0], sv.xstash[10 * kBlockThreads + k0],
+                     sv.xstash[11 * kBlockThreads + k0]};
+        const f3 dc = dl2 + cs;
+        float* st = sv.xstash;
+        const uint32_t k = threadIdx.x;
+        st[9 * kBlockThreads + k] = dc.x;
+        st[10 * kBlockThreads + k] = dc.y;
+        st[11 * kBlockThreads + k] = dc.z;
+    }
     for (uint32_t i = 0; i < S; ++i) {  // VNDF sampling (:593-623)
         const float4 u = tab[3 * i + 2];
         const MisHit x = load_x(sv, xid);
@@ -305,18 +322,23 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float w = power_h(v_pdf, dl_pdf, cos_pdf, nS);
         vn = vn + continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w);
     }
+    const uint32_t k = opaque_lane_slot();
+    const f3 dc{sv.xstash[9 * kBlockThreads + k], sv.xstash[10 * kBlockThreads + k],
+                sv.xstash[11 * kBlockThreads + k]};
     const f3 sum = dc + vn;
     return f3{sum.x / nS, sum.y / nS, sum.z / nS};
 }
 
 }  // namespace
 
+#ifndef RT_MIS_LANES
+#define RT_MIS_LANES 2  // lanes per pixel (1, 2, 4 or 8)
+#endif
 #ifndef RT_MIS_WAVES_PER_EU
-// 4 waves/SIMD: the kernel fits its 120 VGPRs without scratch (HBM traffic
-// 10.3 MB per 800x600 frame = 1.08x the output bytes); 5 waves ran 23.5 ms
-// with 40 spilled VGPRs (467 MB/frame), 6 waves 22.8 ms with 54 (765 MB/frame),
-// 4 waves 24.3 ms
-#define RT_MIS_WAVES_PER_EU 4
+// 6 waves/SIMD: 75 VGPRs without scratch since the primary hit, the pixel sum
+// and dl/dc wait in the per-lane LDS stash (round 2: 120 VGPRs at 4 waves;
+// 6 waves then spilled 54 VGPRs).  7 waves spills 3
+#define RT_MIS_WAVES_PER_EU 6
 #endif
 template <int GEO>
 __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel(MisParams P) {
@@ -364,59 +386,108 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
         sv.xstash = reinterpret_cast<float*>(lds);
     }
 
-    // pixel of a lane; recomputed from an opaque threadIdx where it is used
-    // (as in rt_kernel.hip), not held across the camera-ray loop
+    // ML lanes per pixel: lane `sub` traces the camera rays i = r*ML + sub of
+    // round r, and the pixel's group leader adds the ML results to the pixel's
+    // sum in ray order i (the same additions as one lane per pixel, :652-677).
+    // Twice the waves of one lane per pixel, each half as long: the 800x600
+    // frame's 7,500 one-lane waves filled the GPU's wave slots 1.8 times over,
+    // the second time only partly.
+    // Pixel of a lane; recomputed from an opaque threadIdx where it is used
+    // (as in rt_kernel.hip), not held across the camera-ray loop.  A wave is
+    // 8 x (8 / ML) pixels, a workgroup 2 x 2 waves.
+    constexpr uint32_t ML = RT_MIS_LANES;
+    constexpr uint32_t kWY = 8u / ML;
     auto pixel_of = [&](uint32_t tid, uint32_t& x, uint32_t& j) {
-        const uint32_t lane = tid & 63u, wave = tid >> 6;
-        x = blockIdx.x * kTile + (wave & 1u) * 8u + (lane & 7u);
-        j = blockIdx.y * kTile + (wave >> 1) * 8u + (lane >> 3);
+        const uint32_t lane = tid & 63u, wave = tid >> 6, pix = lane / ML;
+        x = blockIdx.x * 16u + (wave & 1u) * 8u + (pix & 7u);
+        j = blockIdx.y * (2u * kWY) + (wave >> 1) * kWY + (pix >> 3);
     };
     {
         uint32_t x, j;
         pixel_of(threadIdx.x, x, j);
-        if (x >= (uint32_t)P.W || j >= P.row_count) return;
+        if (x >= (uint32_t)P.W || j >= P.row_count) return;  // a pixel's ML lanes leave together
     }
     const f3 cu{P.cam_u[0], P.cam_u[1], P.cam_u[2]}, cv{P.cam_v[0], P.cam_v[1], P.cam_v[2]};
     const f3 cw{P.cam_w[0], P.cam_w[1], P.cam_w[2]};
     const f3 cpos{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
     const float fW = (float)P.W, fH = (float)P.H;
-    f3 acc{0.0f, 0.0f, 0.0f};
-    for (uint32_t i = 0; i < P.camera_rays; ++i) {  // :652
-        uint32_t x, j;
-        pixel_of(opaque_u32(threadIdx.x), x, j);
-        const uint32_t y = P.row_start + j * P.row_step;
-        const float fx = (float)x, fy = (float)y;
-        // hashRandom(index, i) (:71-85); the 800 is the reference's hard-coded width
-        const uint32_t sample_id = (y * 800u + x) * i;
-        const float jx = mis_unit(mis_hash(x + y * 800u + sample_id));
-        const float jy = mis_unit(mis_hash(y + x * 600u + sample_id + 12345u));
-        // generateCameraRay (:214-246)
-        const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
-        const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
-        const float sh = sx * P.halfW, th = ty * P.halfH;
-        const f3 d = normalize((cu * sh + cv * th) - cw);
-        float t;
-        const int id = mis_closest<GEO>(sv, cpos, d, 1000.0f, &t);
-        if (id < 0) continue;                               // Miss (:665)
-        const float4 r0 = sv.shade[3 * id];
-        if (r0.w != 0.0f) {                                 // HitLight (:667-671)
-            acc = acc + f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
-            continue;
-        }
-        {  // the primary hit x into this lane's stash
-            const f3 hp = cpos + d * t;
-            float* st = sv.xstash;
-            const uint32_t k = threadIdx.x;
-            st[k] = hp.x;
-            st[kBlockThreads + k] = hp.y;
-            st[2 * kBlockThreads + k] = hp.z;
-            st[3 * kBlockThreads + k] = d.x;
-            st[4 * kBlockThreads + k] = d.y;
-            st[5 * kBlockThreads + k] = d.z;
-        }
-        acc = acc + mis_shade_hit<GEO>(P, sv, (uint32_t)id);  // :674-676
+    // the pixel's running sum lives in the lane's stash slots 6-8 between rounds
+    // (kept out of the registers the nested MIS queries need)
+    {
+        float* st = sv.xstash;
+        const uint32_t k = threadIdx.x;
+        st[6 * kBlockThreads + k] = 0.0f;
+        st[7 * kBlockThreads + k] = 0.0f;
+        st[8 * kBlockThreads + k] = 0.0f;
     }
+    const uint32_t rounds = (P.camera_rays + ML - 1u) / ML;
+    for (uint32_t r = 0; r < rounds; ++r) {  // :652
+        const uint32_t tid = opaque_u32(threadIdx.x);
+        const uint32_t sub = tid % ML;
+        const uint32_t i = r * ML + sub;
+        f3 c{0.0f, 0.0f, 0.0f};
+        bool has = false;  // Miss (:665), or a ray past camera_rays: nothing to add
+        if (i < P.camera_rays) {
+            uint32_t x, j;
+            pixel_of(tid, x, j);
+            const uint32_t y = P.row_start + j * P.row_step;
+            const float fx = (float)x, fy = (float)y;
+            // hashRandom(index, i) (:71-85); the 800 is the reference's hard-coded width
+            const uint32_t sample_id = (y * 800u + x) * i;
+            const float jx = mis_unit(mis_hash(x + y * 800u + sample_id));
+            const float jy = mis_unit(mis_hash(y + x * 600u + sample_id + 12345u));
+            // generateCameraRay (:214-246)
+            const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
+            const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
+            const float sh = sx * P.halfW, th = ty * P.halfH;
+            const f3 d = normalize((cu * sh + cv * th) - cw);
+            float t;
+            const int id = mis_closest<GEO>(sv, cpos, d, 1000.0f, &t);
+            if (id >= 0) {
+                const float4 r0 = sv.shade[3 * id];
+                has = true;
+                if (r0.w != 0.0f) {                         // HitLight (:667-671)
+                    c = f3{P.l_radiance[0], P.l_radiance[1], P.l_radiance[2]};
+                } else {
+                    {  // the primary hit x into this lane's stash
+                        const f3 hp = cpos + d * t;
+                        float* st = sv.xstash;
+                        const uint32_t k = threadIdx.x;
+                        st[k] = hp.x;
+                        st[kBlockThreads + k] = hp.y;
+                        st[2 * kBlockThreads + k] = hp.z;
+                        st[3 * kBlockThreads + k] = d.x;
+                        st[4 * kBlockThreads + k] = d.y;
+                        st[5 * kBlockThreads + k] = d.z;
+                    }
+                    c = mis_shade_hit<GEO>(P, sv, (uint32_t)id);  // :674-676
+                }
+            }
+        }
+        const uint32_t t2 = opaque_u32(threadIdx.x);
+        float* st = sv.xstash;
+        f3 acc{st[6 * kBlockThreads + t2], st[7 * kBlockThreads + t2], st[8 * kBlockThreads + t2]};
+        if (ML == 1) {
+            if (has) acc = acc + c;
+        } else {  // in ray order: lane base + k holds ray r*ML + k
+            const int base = (int)((t2 & 63u) - t2 % ML);
+#pragma unroll
+            for (uint32_t k = 0; k < ML; ++k) {
+                const f3 ck{__shfl(c.x, base + (int)k), __shfl(c.y, base + (int)k),
+                            __shfl(c.z, base + (int)k)};
+                const bool hk = __shfl((int)has, base + (int)k) != 0;
+                if (hk) acc = acc + ck;  // every lane of the group keeps the same sum
+            }
+        }
+        st[6 * kBlockThreads + t2] = acc.x;
+        st[7 * kBlockThreads + t2] = acc.y;
+        st[8 * kBlockThreads + t2] = acc.z;
+    }
+    const uint32_t tl = opaque_u32(threadIdx.x);
+    const f3 acc{sv.xstash[6 * kBlockThreads + tl], sv.xstash[7 * kBlockThreads + tl],
+                 sv.xstash[8 * kBlockThreads + tl]};
     const float nc = (float)P.camera_rays;
+    if (opaque_u32(threadIdx.x) % ML != 0) return;  // the group leader stores the pixel
     uint32_t x, j;
     pixel_of(opaque_u32(threadIdx.x), x, j);
     const size_t o = (size_t)j * (size_t)P.W + x;
@@ -436,14 +507,15 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     }
 }
 
-constexpr size_t kMisStashBytes = 6u * kBlockThreads * sizeof(float);  // per-lane primary hit (p, din)
+constexpr size_t kMisStashBytes = 12u * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc
 
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + shading records
     return (size_t)((n_pairs ? kPairF4 * n_pairs : 3u * n_tri) + 3u * n_tri) * sizeof(float4);
 }
 
 hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
-    const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
+    constexpr uint32_t TY = 2u * (8u / RT_MIS_LANES);  // workgroup: 16 x TY pixels
+    const dim3 grid((P.W + 15u) / 16u, (P.row_count + TY - 1) / TY);
     const bool pairs = mem != SceneMem::kLdsSingle && P.nP > 0;
     const size_t lds = mis_lds_bytes(P.nT, pairs ? P.nP : 0u);
     const bool lds_ok = mem != SceneMem::kSmem && lds <= kMaxLdsBytes;
