@@ -645,7 +645,8 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
                                            std::min(lds_pairs, lds_single) > rt::kMaxLdsBytes)));
         if (need_bvh) {
             const size_t nn = 2 * (size_t)nT - 1;
-            if ((e = hipMalloc((void**)&c->d_tri_nodes, 8 * nn * 2 * sizeof(float4))) != hipSuccess ||
+            // 8 layouts of 32-B nodes, then 2 compact layouts of 16-B entries (rt_lbvh.hip)
+            if ((e = hipMalloc((void**)&c->d_tri_nodes, (8 * nn * 2 + RT_TRI_COMPACT_LAYOUTS * nn) * sizeof(float4))) != hipSuccess ||
                 (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
                 (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
                 status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;

@@ -40,6 +40,12 @@ inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t b
 #endif
 constexpr uint32_t kSphBlockThreads = RT_SPH_BLOCK;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
+// Compact layouts of the triangle BVH (rt_lbvh.hip, rt_trace.hpp tri_cbvh_*): 2
+// (octants +++ and ---, rays take the majority of their signs) or 8 (one per
+// direction octant), 16 B per node, stored after the 8 full 32-B layouts.
+#ifndef RT_TRI_COMPACT_LAYOUTS
+#define RT_TRI_COMPACT_LAYOUTS 8
+#endif
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
 constexpr uint32_t kTriBvhMinTriangles = 384;

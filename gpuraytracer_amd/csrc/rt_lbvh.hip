@@ -11,6 +11,7 @@
 // near child first along the node's split axis, every box padded by the
 // culling margin.  One triangle per leaf.  Only speed depends on the tree: the
 // walks in rt_trace.hpp return the brute-force (t, id) minimum.
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -156,6 +157,20 @@ __global__ void layout_kernel(uint32_t n, const uint32_t* __restrict__ child,
     float4* o = nodes + 2 * ((size_t)oct * total + idx);
     o[0] = make_float4(b0.x, b0.y, b0.z, __uint_as_float(escape));
     o[1] = make_float4(b1.x, b1.y, b1.z, __uint_as_float(leaf));
+    if (RT_TRI_COMPACT_LAYOUTS == 8 || oct == 0 || oct == 7) {
+        // compact 16-B entries (every octant's layout, or only those of (+,+,+)
+        // and (-,-,-)), after the 8 full layouts (rt_trace.hpp tri_cbvh_*): the box in fp16 rounded
+        // outward (a superset of the padded box), then escape | 2^31 for an
+        // inner node (an entry index over all compact layouts) or the leaf's triangle
+        // index in leaf order (a leaf's escape is the next entry)
+        const uint32_t lay = RT_TRI_COMPACT_LAYOUTS == 8 ? oct : (oct == 7 ? 1u : 0u);
+        uint4* cn = reinterpret_cast<uint4*>(nodes + 2 * (size_t)8 * total) + (size_t)lay * total + idx;
+        const uint32_t h0 = __half_as_ushort(__float2half_rd(b0.x)), h1 = __half_as_ushort(__float2half_rd(b0.y));
+        const uint32_t h2 = __half_as_ushort(__float2half_rd(b0.z)), h3 = __half_as_ushort(__float2half_ru(b1.x));
+        const uint32_t h4 = __half_as_ushort(__float2half_ru(b1.y)), h5 = __half_as_ushort(__float2half_ru(b1.z));
+        const uint32_t w = (v >= n - 1) ? (v - (n - 1)) : ((lay * total + escape) | 0x80000000u);
+        *cn = make_uint4(h0 | (h1 << 16), h2 | (h3 << 16), h4 | (h5 << 16), w);
+    }
 }
 
 __global__ void gather_kernel(const float4* __restrict__ tri, const uint32_t* __restrict__ ids,

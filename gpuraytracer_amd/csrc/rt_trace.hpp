@@ -748,6 +748,80 @@ __device__ __forceinline__ bool tri_bvh_any(const float4* __restrict__ node,
     return found;
 }
 
+// Triangle-BVH walks over the compact entries (rt_lbvh.hip: 16 B per node, fp16
+// boxes rounded outward, two layouts -- near child first for (+,+,+) and for
+// (-,-,-), a ray takes the one matching most of its direction signs -- stored
+// after the 8 full layouts): the same stackless depth-first walks, conservative
+// boxes and (t, id) ranking as tri_bvh_*, with half the bytes per step and a
+// quarter of the layouts in the caches.
+__device__ __forceinline__ const uint4* tri_compact(const float4* node, uint32_t nN) {
+    return reinterpret_cast<const uint4*>(node + 16u * nN);
+}
+__device__ __forceinline__ uint32_t tri_compact_layout(f3 d) {
+    return RT_TRI_COMPACT_LAYOUTS == 8 ? octant(d) : lds_layout(d);
+}
+
+template <bool PACKET>
+__device__ __forceinline__ void tri_cbvh_closest(const uint4* __restrict__ cn,
+                                                 const float4* __restrict__ tri,
+                                                 const uint32_t* __restrict__ perm, uint32_t nN,
+                                                 f3 o, f3 d, float tmin, float& best, int& id) {
+    const RayBox rb = ray_box(o, d);
+    uint32_t idx = (PACKET ? wave_uniform(tri_compact_layout(d)) : tri_compact_layout(d)) * nN;
+    const uint32_t end = idx + nN;
+    while (idx < end) {
+        const uint4 e = cn[idx];
+        const bool inner = (e.w & 0x80000000u) != 0u;  // wave-uniform for PACKET
+        const bool h = lds_node_hit(e, rb, tmin, best);
+        uint32_t next = idx + 1;
+        if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) {
+            if (inner) next = e.w & 0x7FFFFFFFu;
+        } else if (!inner) {
+            const uint32_t k = e.w;
+            float t;
+            if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f, &t) &&
+                t <= best) {
+                const int tid = (int)perm[k];
+                if (t < best || tid < id) {
+                    best = t;
+                    id = tid;
+                }
+            }
+        }
+        idx = PACKET ? wave_uniform(next) : next;
+    }
+}
+
+template <bool PACKET>
+__device__ __forceinline__ bool tri_cbvh_any(const uint4* __restrict__ cn, const float4* __restrict__ tri,
+                                             uint32_t nN, f3 o, f3 d, float tmin, float tmax) {
+    const RayBox rb = ray_box(o, d);
+    uint32_t idx = (PACKET ? wave_uniform(tri_compact_layout(d)) : tri_compact_layout(d)) * nN;
+    const uint32_t end = idx + nN;
+    bool found = false;
+    while (idx < end) {
+        const uint4 e = cn[idx];
+        const bool inner = (e.w & 0x80000000u) != 0u;
+        const bool h = !found && lds_node_hit(e, rb, tmin, tmax);
+        uint32_t next = idx + 1;
+        if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) {
+            if (inner) next = e.w & 0x7FFFFFFFu;
+        } else if (!inner) {
+            const uint32_t k = e.w;
+            float t;
+            found = found || tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax, &t);
+            if (!PACKET && found) return true;
+            if (PACKET && __builtin_amdgcn_ballot_w64(!found) == 0) break;
+        }
+        idx = PACKET ? wave_uniform(next) : next;
+    }
+    return found;
+}
+
+#ifndef RT_TRI_COMPACT
+#define RT_TRI_COMPACT 1  // triangle-BVH walks over the compact 16-B entries
+#endif
+
 // ---- box clusters ------------------------------------------
 // Candidate pairs of one ray among the clustered pairs: bit k set when pair k
 // can hold an accepted hit with t in (tmin, tmax).  Per cluster: slab test of
@@ -986,7 +1060,11 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
             }
         }
     } else if (GEO == kGeoTriBvh) {
-        tri_bvh_closest<CULL>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin, best, id);
+        if (RT_TRI_COMPACT)
+            tri_cbvh_closest<CULL>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d,
+                                   tmin, best, id);
+        else
+            tri_bvh_closest<CULL>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin, best, id);
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
             float t;
@@ -1047,7 +1125,10 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
             }
         }
     } else if (GEO == kGeoTriBvh) {
-        if (tri_bvh_any<PACKET>(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax)) return true;
+        if (RT_TRI_COMPACT ? tri_cbvh_any<PACKET>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o, d,
+                                                  tmin, tmax)
+                           : tri_bvh_any<PACKET>(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax))
+            return true;
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
             float t;
