@@ -439,6 +439,9 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
 // is positive -- and every lane reads back its own query's result.  Extra
 // entries visited by a split walk can only add candidates that are real hits
 // in (tmin, tmax), so the minimum is the brute-force one.
+#ifndef RT_SPH_PARK_DEN
+#define RT_SPH_PARK_DEN 2  // the parked roots run once they are >= 1/DEN of the live lanes
+#endif
 #ifndef RT_SPH_SPLIT_CLOSEST_ONLY
 #define RT_SPH_SPLIT_CLOSEST_ONLY 0  // 1: shadow (any-hit) walks are not split
 #endif
@@ -514,7 +517,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             }
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
-            if (2 * parked >= live) break;
+            if (RT_SPH_PARK_DEN * parked >= live) break;
             if constexpr (SPLIT) {
                 if (n_exec - live >= split_at) {  // lanes with nothing to walk
                     RT_STAT(ST + 4, 1);
@@ -818,6 +821,72 @@ __device__ __forceinline__ bool tri_cbvh_any(const uint4* __restrict__ cn, const
     return found;
 }
 
+// Per-lane compact-BVH walks with POSTPONED LEAVES (as sphere_walk_lds parks
+// its roots): a lane whose box test passes at a leaf parks the triangle and
+// stops; the others walk on until at least half of the lanes still walking
+// are parked, then the wave runs the triangle tests of all parked lanes
+// together -- instead of every mixed step paying for the box test AND the
+// three record loads and the test of a triangle.  Per lane the entries are
+// visited in the same order and ranked by (t, id): the same result.
+#ifndef RT_TRI_PARK_DEN
+#define RT_TRI_PARK_DEN 4  // the parked leaves are tested once they are >= 1/DEN of the live lanes
+#endif
+template <bool ANY>
+__device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, const float4* __restrict__ tri,
+                                              const uint32_t* __restrict__ perm, uint32_t nN, f3 o, f3 d,
+                                              float tmin, float& best, int& id) {
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const RayBox rb = ray_box(o, d);
+    uint32_t idx = tri_compact_layout(d) * nN;
+    const uint32_t end = idx + nN;
+    if (ANY && id >= 0) idx = end;
+    uint32_t leaf = kNone;
+    for (;;) {
+        for (;;) {
+            const bool adv = idx < end && leaf == kNone;
+            if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
+            if (adv) {
+                const uint4 e = cn[idx];
+                const bool inner = (e.w & 0x80000000u) != 0u;
+                if (!lds_node_hit(e, rb, tmin, best)) {
+                    idx = inner ? (e.w & 0x7FFFFFFFu) : idx + 1;
+                } else {
+                    if (!inner) leaf = e.w;
+                    idx = idx + 1;
+                }
+            }
+            const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
+            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
+            if (RT_TRI_PARK_DEN * parked >= live) break;
+        }
+        if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
+        if (leaf != kNone) {
+            float t;
+            if (tri_test(tri[3 * leaf], tri[3 * leaf + 1], tri[3 * leaf + 2], o, d, tmin,
+                         ANY ? best : 3.0e38f, &t)) {
+                if (ANY) {
+                    id = 0;
+                    idx = end;
+                } else if (t <= best) {
+                    const int tid = (int)perm[leaf];
+                    if (t < best || tid < id) {
+                        best = t;
+                        id = tid;
+                    }
+                }
+            }
+            leaf = kNone;
+        }
+    }
+}
+
+#ifndef RT_TRI_PARK
+#define RT_TRI_PARK 1  // per-lane triangle-BVH walks with postponed leaves (tri_cbvh_walk)
+#endif
+#ifndef RT_TRI_PARK_ALL
+#define RT_TRI_PARK_ALL 0  // 1: also camera and bounce-0 shadow rays (else wave-packet walks)
+#endif
+
 #ifndef RT_TRI_COMPACT
 #define RT_TRI_COMPACT 1  // triangle-BVH walks over the compact 16-B entries
 #endif
@@ -1060,7 +1129,10 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
             }
         }
     } else if (GEO == kGeoTriBvh) {
-        if (RT_TRI_COMPACT)
+        if (RT_TRI_COMPACT && RT_TRI_PARK && (!CULL || RT_TRI_PARK_ALL))
+            tri_cbvh_walk<false>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+                                 best, id);
+        else if (RT_TRI_COMPACT)
             tri_cbvh_closest<CULL>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d,
                                    tmin, best, id);
         else
@@ -1125,10 +1197,17 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
             }
         }
     } else if (GEO == kGeoTriBvh) {
-        if (RT_TRI_COMPACT ? tri_cbvh_any<PACKET>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o, d,
-                                                  tmin, tmax)
-                           : tri_bvh_any<PACKET>(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax))
+        if (RT_TRI_COMPACT && RT_TRI_PARK && (!PACKET || RT_TRI_PARK_ALL)) {
+            float tm = tmax;
+            int hid = -1;
+            tri_cbvh_walk<true>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+                                tm, hid);
+            if (hid >= 0) return true;
+        } else if (RT_TRI_COMPACT ? tri_cbvh_any<PACKET>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o,
+                                                         d, tmin, tmax)
+                                  : tri_bvh_any<PACKET>(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax)) {
             return true;
+        }
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
             float t;

@@ -35,9 +35,12 @@ def bench_workload(argv):
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--spheres", type=int, default=1000)
+    ap.add_argument("--triangles", type=int, default=100000)
     a, _ = ap.parse_known_args(argv)
     if a.scene == "cornell":
         return f"cornell_{a.width}x{a.height}_{a.spp}spp_b{a.bounces}"
+    if a.scene == "triangles":
+        return f"triangles{a.triangles}_{a.width}x{a.height}_{a.spp}spp_b{a.bounces}"
     return f"spheres{a.spheres}_{a.width}x{a.height}_{a.spp}spp_b{a.bounces}"
 
 
