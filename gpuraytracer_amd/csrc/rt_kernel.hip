@@ -386,7 +386,10 @@ void path_trace_kernel(KParams P) {
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
-        if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) after the pairs
+        if (GEO == kGeoSphLds && RT_SPH_LAYOUTS == 8) {  // 8 compact layouts: global (L2)
+            sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
+            sv.sid = P.sph_lds_id;
+        } else if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) after the pairs
             const uint32_t ne = 2u * P.nE;
             const uint4* es = reinterpret_cast<const uint4*>(P.sph_lds);
             uint4* ed = reinterpret_cast<uint4*>(lds + ng4);

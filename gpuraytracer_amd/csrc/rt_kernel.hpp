@@ -27,9 +27,16 @@ constexpr size_t kSphLdsMaxBytes = 73 * 1024;
 #define RT_SPH_SPLIT 0  // measured: wave steps -40 %, no faster; opt-in
 #endif
 constexpr uint32_t kWaveScratchBytes = 576;
+// Layouts of the compact sphere BVH (rt_scene.cpp build_sphere_lds): 2 --
+// octants (+,+,+) and (-,-,-), staged in LDS -- or 8, one per direction
+// octant, too big for LDS and read from global memory (L2) instead.
+#ifndef RT_SPH_LAYOUTS
+#define RT_SPH_LAYOUTS 2
+#endif
 // dynamic LDS of the LDS-sphere kernel: pair records, both layouts of the
 // compact BVH, then the wave scratch (RT_SPH_SPLIT) or the entry ids
 inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t block_threads) {
+    if (RT_SPH_LAYOUTS == 8) return pair_bytes;  // entries and ids stay in global memory
     const size_t ent = 2u * (size_t)n_entries * 16u;
     return pair_bytes + ent +
            (RT_SPH_SPLIT ? (size_t)(block_threads / 64u) * kWaveScratchBytes

@@ -8,6 +8,7 @@
 #include <algorithm>
 
 #include "../../include/rtpt.h"
+#include "rt_kernel.hpp"
 
 namespace rt {
 
@@ -434,10 +435,13 @@ static void build_sphere_lds(CompiledScene* out) {
     if (ne > 0x7FFFu) return;
     std::vector<uint32_t> ent;
     std::vector<uint16_t> ids;
-    for (int oct : {0, 7}) {
-        // escapes are entry indices of the concatenated layouts (layout 1
-        // starts at ne), so a walk's position alone names its layout
-        const uint32_t lay_base = oct == 0 ? 0u : ne;
+    const int octs2[2] = {0, 7}, octs8[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+    const int nlay = RT_SPH_LAYOUTS == 8 ? 8 : 2;
+    for (int li = 0; li < nlay; ++li) {
+        const int oct = nlay == 8 ? octs8[li] : octs2[li];
+        // escapes are entry indices of the concatenated layouts (layout li
+        // starts at li * ne), so a walk's position alone names its layout
+        const uint32_t lay_base = (uint32_t)li * ne;
         const BvhNode* L = out->sph_nodes.data() + (size_t)oct * nn;
         uint32_t k = 0;  // running entry index of this layout
         std::vector<uint32_t> lpos(nn + 1);

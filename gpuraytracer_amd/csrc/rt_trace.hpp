@@ -367,6 +367,8 @@ __device__ __forceinline__ uint32_t lds_layout(f3 d) {
 #endif
     return __builtin_popcount(octant(d)) >= 2 ? 1u : 0u;
 }
+// layout of the compact sphere BVH a ray walks (RT_SPH_LAYOUTS)
+__device__ __forceinline__ uint32_t sph_layout(f3 d) { return RT_SPH_LAYOUTS == 8 ? octant(d) : lds_layout(d); }
 
 __device__ __forceinline__ bool lds_node_hit(const uint4& e, const RayBox& rb, float tmin,
                                              float tmax) {
@@ -381,7 +383,7 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
                                                    float tmin, float& best, int& id) {
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
-    const uint32_t lay = PACKET ? wave_uniform(lds_layout(d)) : lds_layout(d);
+    const uint32_t lay = PACKET ? wave_uniform(sph_layout(d)) : sph_layout(d);
     // entry indices (and escapes) run over both layouts: layout `lay` is
     // [lay * nN, (lay + 1) * nN)
     uint32_t idx = lay * nN;
@@ -440,7 +442,7 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
 // entries visited by a split walk can only add candidates that are real hits
 // in (tmin, tmax), so the minimum is the brute-force one.
 #ifndef RT_SPH_PARK_DEN
-#define RT_SPH_PARK_DEN 2  // the parked roots run once they are >= 1/DEN of the live lanes
+#define RT_SPH_PARK_DEN 4  // the parked roots run once they are >= 1/DEN of the live lanes
 #endif
 #ifndef RT_SPH_SPLIT_CLOSEST_ONLY
 #define RT_SPH_SPLIT_CLOSEST_ONLY 0  // 1: shadow (any-hit) walks are not split
@@ -469,7 +471,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
     float a = dot(d, d);
     RayBox rb = ray_box(o, d);
     // entry range of this lane's walk over the concatenated layouts
-    uint32_t idx = lds_layout(d) * nN;
+    uint32_t idx = sph_layout(d) * nN;
     uint32_t end = idx + nN;
     if (ANY && id >= 0) idx = end;
     uint32_t leaf = kNone;                      // the parked leaf
@@ -641,7 +643,7 @@ __device__ __forceinline__ bool sphere_any_lds(const uint4* ent, uint32_t nN, f3
                                                float tmin, float tmax) {
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
-    const uint32_t lay = PACKET ? wave_uniform(lds_layout(d)) : lds_layout(d);
+    const uint32_t lay = PACKET ? wave_uniform(sph_layout(d)) : sph_layout(d);
     bool found = false;
     uint32_t idx = lay * nN;
     const uint32_t end = idx + nN;

@@ -18,5 +18,7 @@ step gputest 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step prof_cornell 600 bash tools/profile.sh ${TAG}_cornell
 step prof_spheres 600 bash tools/profile.sh ${TAG}_spheres --scene spheres
+step prof_mis 600 env PROFILE_TARGET=mis bash tools/profile.sh ${TAG}_mis
+step prof_tri100k 600 bash tools/profile.sh ${TAG}_tri100k --scene triangles --triangles 100000 --spp 64
 step bench 400 python bench.py
 step spheres 300 python bench.py --scene spheres --steps 8 --warmup 1 --cpu-baseline off
