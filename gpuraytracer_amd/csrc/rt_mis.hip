@@ -22,6 +22,10 @@
 #include "rt_kernel.hpp"
 #include "rt_trace.hpp"
 
+#ifndef RT_MIS_SUM_LDS
+#define RT_MIS_SUM_LDS 1  // the cosine / VNDF strategy sums accumulate in the stash (slots 12-14)
+#endif
+
 namespace rt {
 
 namespace {
@@ -192,6 +196,27 @@ __device__ __forceinline__ MisHit load_x(const SceneView& sv, uint32_t id) {
     return x;
 }
 
+// s[slot..slot+2] += v in this lane's stash (the running strategy sums; the same
+// additions in the same order as a register accumulator)
+__device__ __forceinline__ void stash_add(const SceneView& sv, uint32_t slot, f3 v) {
+    float* st = sv.xstash;
+    const uint32_t k = opaque_lane_slot();
+    st[slot * kBlockThreads + k] = st[slot * kBlockThreads + k] + v.x;
+    st[(slot + 1) * kBlockThreads + k] = st[(slot + 1) * kBlockThreads + k] + v.y;
+    st[(slot + 2) * kBlockThreads + k] = st[(slot + 2) * kBlockThreads + k] + v.z;
+}
+__device__ __forceinline__ f3 stash_get(const SceneView& sv, uint32_t slot) {
+    const uint32_t k = opaque_lane_slot();
+    return f3{sv.xstash[slot * kBlockThreads + k], sv.xstash[(slot + 1) * kBlockThreads + k],
+              sv.xstash[(slot + 2) * kBlockThreads + k]};
+}
+__device__ __forceinline__ void stash_set(const SceneView& sv, uint32_t slot, f3 v) {
+    const uint32_t k = opaque_lane_slot();
+    sv.xstash[slot * kBlockThreads + k] = v.x;
+    sv.xstash[(slot + 1) * kBlockThreads + k] = v.y;
+    sv.xstash[(slot + 2) * kBlockThreads + k] = v.z;
+}
+
 // calculateDirectLightSamplingContribution (:519-541).  POWER: MIS-weighted
 // (first hit) or plain (at the secondary hit, samplesPerStrategy = 1).  The
 // contribution is formed BEFORE the visibility query (the same operations:
@@ -280,6 +305,7 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         st[10 * kBlockThreads + k] = dl.y;
         st[11 * kBlockThreads + k] = dl.z;
     }
+    if (RT_MIS_SUM_LDS) stash_set(sv, 12, f3{0.0f, 0.0f, 0.0f});
     for (uint32_t i = 0; i < S; ++i) {  // cosine-hemisphere sampling (:562-591)
         const float4 u = tab[3 * i + 1];
         const MisHit x = load_x(sv, xid);
@@ -293,8 +319,13 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float dl_pdf = light_pdf(P, x.p, dir);
         const float v_pdf = vndf_pdf(V, n, dir, hit_m(sv, x).roughness);
         const float w = power_h(cos_pdf, dl_pdf, v_pdf, nS);
+#if RT_MIS_SUM_LDS
+        stash_add(sv, 12, continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w));
+#else
         cs = cs + continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w);
+#endif
     }
+    if (RT_MIS_SUM_LDS) cs = stash_get(sv, 12);
     {  // (directLight + cosine) + vndf (:624), same order; dc waits in the stash
         const uint32_t k0 = opaque_lane_slot();
         const f3 dl2{sv.xstash[9 * kBlockThreads + k0], sv.xstash[10 * kBlockThreads + k0],
@@ -306,6 +337,7 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         st[10 * kBlockThreads + k] = dc.y;
         st[11 * kBlockThreads + k] = dc.z;
     }
+    if (RT_MIS_SUM_LDS) stash_set(sv, 12, f3{0.0f, 0.0f, 0.0f});
     for (uint32_t i = 0; i < S; ++i) {  // VNDF sampling (:593-623)
         const float4 u = tab[3 * i + 2];
         const MisHit x = load_x(sv, xid);
@@ -320,8 +352,13 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float cos_pdf = cosine_pdf(n, dir);
         const float dl_pdf = light_pdf(P, x.p, dir);
         const float w = power_h(v_pdf, dl_pdf, cos_pdf, nS);
+#if RT_MIS_SUM_LDS
+        stash_add(sv, 12, continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w));
+#else
         vn = vn + continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w);
+#endif
     }
+    if (RT_MIS_SUM_LDS) vn = stash_get(sv, 12);
     const uint32_t k = opaque_lane_slot();
     const f3 dc{sv.xstash[9 * kBlockThreads + k], sv.xstash[10 * kBlockThreads + k],
                 sv.xstash[11 * kBlockThreads + k]};
@@ -335,10 +372,10 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
 #define RT_MIS_LANES 2  // lanes per pixel (1, 2, 4 or 8)
 #endif
 #ifndef RT_MIS_WAVES_PER_EU
-// 6 waves/SIMD: 75 VGPRs without scratch since the primary hit, the pixel sum
-// and dl/dc wait in the per-lane LDS stash (round 2: 120 VGPRs at 4 waves;
-// 6 waves then spilled 54 VGPRs).  7 waves spills 3
-#define RT_MIS_WAVES_PER_EU 6
+// 7 waves/SIMD: 72 VGPRs without scratch since the primary hit, the pixel sum,
+// dl/dc and the running strategy sum wait in the per-lane LDS stash (round 2:
+// 120 VGPRs at 4 waves; 6 waves then spilled 54 VGPRs).  DESIGN.md §5
+#define RT_MIS_WAVES_PER_EU 7
 #endif
 template <int GEO>
 __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel(MisParams P) {
@@ -507,7 +544,7 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     }
 }
 
-constexpr size_t kMisStashBytes = 12u * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc
+constexpr size_t kMisStashBytes = (RT_MIS_SUM_LDS ? 15u : 12u) * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc (+ strategy sum)
 
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + shading records
     return (size_t)((n_pairs ? kPairF4 * n_pairs : 3u * n_tri) + 3u * n_tri) * sizeof(float4);
