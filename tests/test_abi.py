@@ -188,3 +188,40 @@ def test_bench_multi_gpu_launcher_needs_the_gpus():
                        env=dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES=""))
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
+
+
+def test_c_program_links_the_abi(tmp_path):
+    """A plain C99 program (what a Swift / cgo / JNI shim compiles against)
+    includes rtpt.h, links librtpt.so and calls the host-only entry points:
+    the tile layout of the multi-GPU gather and its host placement."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "abi.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <string.h>
+#include "rtpt.h"
+int main(void) {
+    rt_tile_layout_info a, b;
+    if (rt_tile_layout(6, 5, 2, 0, 0, &a) || rt_tile_layout(6, 5, 2, 1, RT_OUT_RGBA8, &b)) return 1;
+    if (a.rows != 3 || a.rows_max != 3 || a.row_bytes != 96 || a.tile_bytes != 288) return 2;
+    if (b.rows != 2 || b.row_bytes != 24 || b.tile_bytes != 72) return 3;
+    unsigned char g[2 * 72], f[5 * 24];
+    for (int i = 0; i < (int)sizeof g; ++i) g[i] = (unsigned char)i;
+    if (rt_place_tiles_host(g, 6, 5, 2, RT_OUT_RGBA8, f)) return 4;
+    /* frame row 1 = rank 1's tile row 0, row 4 = rank 0's tile row 2 */
+    if (memcmp(f + 24, g + 72, 24) || memcmp(f + 4 * 24, g + 48, 24)) return 5;
+    if (rt_abi_version() != RTPT_ABI_VERSION) return 6;
+    printf("ok\n");
+    return 0;
+}
+''')
+    exe = tmp_path / "abi"
+    libdir = os.path.join(ROOT, "gpuraytracer_amd")
+    subprocess.check_call([cc, "-std=c99", "-Wall", "-I", os.path.join(ROOT, "include"), str(src),
+                           "-o", str(exe), "-L", libdir, "-lrtpt", "-Wl,-rpath," + libdir])
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", (out.returncode, out.stderr[-500:])
