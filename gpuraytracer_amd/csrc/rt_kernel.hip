@@ -192,6 +192,32 @@ __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv
     }
 }
 
+// In-order sum of the L colours of a pixel's lanes at its group leader, with
+// DPP row shifts (row_shl:k: lane i reads lane i + k of its 16-lane row).
+#ifndef RT_DPP_SUM
+#define RT_DPP_SUM 1
+#endif
+template <int k>
+__device__ __forceinline__ float row_shl(float v) {
+    if constexpr (k == 0) {
+        return v;
+    } else {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + k, 0xF, 0xF, false));
+    }
+}
+template <int L, int k>
+struct row_sum_in_order {
+    __device__ __forceinline__ static void run(f3& acc, f3 c, uint32_t n0, uint32_t spp) {
+        if (n0 + (uint32_t)k < spp)  // wave-uniform: the round's last samples may be past spp
+            acc = acc + f3{row_shl<k>(c.x), row_shl<k>(c.y), row_shl<k>(c.z)};
+        row_sum_in_order<L, k + 1>::run(acc, c, n0, spp);
+    }
+};
+template <int L>
+struct row_sum_in_order<L, L> {
+    __device__ __forceinline__ static void run(f3&, f3, uint32_t, uint32_t) {}
+};
+
 // The pixel store (raytrace.metal:109): float4(luminance, 1) as rgba32F, as
 // the reference's rgba16F texture (renderer.swift:74-82), or that texture
 // tonemapped to the reference's 8-bit image (RTrace/image.swift:35-65: fp16
@@ -539,6 +565,21 @@ void path_trace_kernel(KParams P) {
         }
         if (L == 1) {
             lum = lum + s.acc;                                   // :103
+        } else if (RT_DPP_SUM && L <= 16 && !SPH) {  // (the sphere kernel keeps ds_bpermute:
+                                                       //  the DPP form spills 3 more VGPRs there)
+            // a pixel's L lanes are consecutive lanes of one 16-lane DPP row
+            // (L = 4: groups at 0, 4, 8, 12; L = 16: the whole row), so its
+            // leader reads sample r*L + k from lane +k with a row shift fused
+            // into the add (v_add_f32_dpp row_shl:k) -- the same additions in
+            // sample order, no LDS-pipe traffic.  Only the leaders' sums are kept.
+            const uint32_t t2 = opaque_tid(), sub2 = t2 % L, slot = t2 / L;
+            f3 acc{lum_s[3 * slot], lum_s[3 * slot + 1], lum_s[3 * slot + 2]};
+            row_sum_in_order<L, 0>::run(acc, s.acc, r * L, P.spp);  // :103
+            if (sub2 == 0) {
+                lum_s[3 * slot] = acc.x;
+                lum_s[3 * slot + 1] = acc.y;
+                lum_s[3 * slot + 2] = acc.z;
+            }
         } else {
             const uint32_t t2 = opaque_tid(), lane = t2 & 63u, sub2 = t2 % L, slot = t2 / L;
             const int base = (int)(lane - sub2);
