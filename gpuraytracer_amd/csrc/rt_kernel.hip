@@ -742,15 +742,21 @@ hipError_t launch_place_tiles(const void* gathered, void* frame, size_t row_byte
 namespace {
 
 // Lanes per pixel (measured on one GPU's share of the N-GPU weak-scaling frame,
-// tools/bench_share.py): 4 for ~1 M pixels and more (also +6 % on the whole
-// 1080p frame: 4x4-pixel waves, more lanes in flight), 16 below that (one GPU's
-// share at N = 4 and 8), never more than spp.  The LDS sphere-walk kernel
+// tools/bench_share.py): 4 for whole frames of ~1 M pixels and more (also +6 % on
+// the whole 1080p frame: 4x4-pixel waves, more lanes in flight), 16 below that
+// and for interleaved shares, never more than spp.  The LDS sphere-walk kernel
 // takes 16 at every size (measured on config 4, the whole 1080p frame: 198.4 ms
 // at 16 lanes, 204.8 at 4, 227.6 at 1).
 inline int lanes_per_pixel(const KParams& P, int geo) {
     if (P.lanes == 1 || P.lanes == 4 || P.lanes == 16) return P.spp >= P.lanes ? (int)P.lanes : 1;
     const uint64_t px = (uint64_t)P.W * P.row_count;
-    const int want = (px >= 1000000ull && geo != kGeoSphLds) ? 4 : 16;
+    // interleaved rows (a rank's share of a multi-GPU frame) take 16 lanes at any
+    // size when every lane still gets the Halton tables' 8 rounds (measured,
+    // tools/lanes_probe.py: 1080p share of N = 2 20,229 vs 19,922; 4096^2 share
+    // of N = 8 19,450 vs 18,824); whole frames of >= 1 M pixels keep 4 (1080p
+    // 20,288 vs 20,143; 4096^2 18,505 vs 17,978)
+    const bool share16 = P.row_step > 1 && P.spp >= 16u * kHaltonTabMinRounds;
+    const int want = (px >= 1000000ull && geo != kGeoSphLds && !share16) ? 4 : 16;
     if (P.spp >= (uint32_t)want) return want;
     return P.spp >= 4 ? 4 : 1;
 }

@@ -97,7 +97,8 @@ def test_c3_rank_share_4096(rank):
         share = r.render(RenderParams(spp=1024, bounces=3, row_start=rank, row_step=8))
         info = r.last_launch()
     assert share.shape == (512, W, 4)
-    assert info["lanes_per_pixel"] == 4 and info["halton_tables"] == 1, info  # 2.1 M pixels
+    # interleaved share: 16 lanes per pixel (64 rounds per lane, tables on)
+    assert info["lanes_per_pixel"] == 16 and info["halton_tables"] == 1, info
     assert np.isfinite(share).all() and np.all(share[..., 3] == 1.0)
     j = 255  # share row j = image row rank + 8 j (mid-frame: boxes, walls)
     ref = oracle_lib.render(s, sd, 1024, 3, row_start=rank + 8 * j, row_step=8, row_count=2,
