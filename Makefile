@@ -12,7 +12,7 @@ BLD ?= build
 COMMON := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude
 HOSTCXX ?= /opt/rocm/llvm/bin/clang++
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-slp-vectorize $(EXTRA)
-HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include
+HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include $(EXTRA)
 
 OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
 HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp $(SRC)/rt_halton.hpp

@@ -68,7 +68,7 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         shading_frame(N, &right, &fwd);
         diffuse = f3{s0.x, s0.y, s0.z};
     }
-    const f3 p = (s.o + s.d * t) + N * 1e-3f;              // :67
+    f3 p = (s.o + s.d * t) + N * 1e-3f;              // :67
 
     // sampleAreaLight (sampling.metal:198-236), dims 2+5b, 3+5b (:72-74)
     const float ux = halton_dim<2 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab) * 2.0f - 1.0f;
@@ -415,6 +415,9 @@ void path_trace_kernel(KParams P) {
         if (GEO == kGeoSphLds && RT_SPH_LAYOUTS == 8) {  // 8 compact layouts: global (L2)
             sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
             sv.sid = P.sph_lds_id;
+            // the walk pool after the pair records (RT_SPH_POOL)
+            sv.pool = reinterpret_cast<uint8_t*>(lds + ng4);
+            if (RT_SPH_POOL) pool_init<NT>(sv.pool, threadIdx.x);
         } else if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) after the pairs
             const uint32_t ne = 2u * P.nE;
             const uint4* es = reinterpret_cast<const uint4*>(P.sph_lds);

@@ -27,15 +27,33 @@ constexpr size_t kSphLdsMaxBytes = 73 * 1024;
 #define RT_SPH_SPLIT 0  // measured: wave steps -40 %, no faster; opt-in
 #endif
 constexpr uint32_t kWaveScratchBytes = 576;
+// Workgroup walk pool (rt_trace.hpp sphere_walk_pool): a
+// wave hands its last sphere walks of a query to an LDS pool that idle lanes
+// of every wave of the workgroup take from.  The pool holds every lane's
+// query slot, so the compact BVH moves to global memory (8 layouts, L2).
+#ifndef RT_SPH_POOL
+#define RT_SPH_POOL 0
+#endif
+#if RT_SPH_POOL && !defined(RT_SPH_LAYOUTS)
+#define RT_SPH_LAYOUTS 8
+#endif
+// pool bytes of one workgroup: per lane 16 B (o, best) + 16 B (d, entry) +
+// 4 B (id + 1, kind), per wave two 64-bit masks (handed over, finished), and
+// one 32-bit summary of the waves with handed-over walks (padded to 16 B)
+inline constexpr size_t sphere_pool_bytes(uint32_t block_threads) {
+    return (size_t)block_threads * 36u + (size_t)(block_threads / 64u) * 16u + 16u;
+}
 // Layouts of the compact sphere BVH (rt_scene.cpp build_sphere_lds): 2 --
 // octants (+,+,+) and (-,-,-), staged in LDS -- or 8, one per direction
 // octant, too big for LDS and read from global memory (L2) instead.
 #ifndef RT_SPH_LAYOUTS
 #define RT_SPH_LAYOUTS 2
 #endif
+static_assert(!RT_SPH_POOL || RT_SPH_LAYOUTS == 8, "the walk pool takes the LDS of the 2-layout tree");
 // dynamic LDS of the LDS-sphere kernel: pair records, both layouts of the
 // compact BVH, then the wave scratch (RT_SPH_SPLIT) or the entry ids
 inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t block_threads) {
+    if (RT_SPH_POOL) return pair_bytes + sphere_pool_bytes(block_threads);
     if (RT_SPH_LAYOUTS == 8) return pair_bytes;  // entries and ids stay in global memory
     const size_t ent = 2u * (size_t)n_entries * 16u;
     return pair_bytes + ent +

@@ -164,6 +164,7 @@ struct SceneView {
     const uint4* sent;        // compact sphere BVH entries in LDS (kGeoSphLds), 2 layouts
     const uint16_t* sid;      // sphere id of each entry (leaves): LDS, or global with RT_SPH_SPLIT
     uint8_t* wscr;            // this wave's LDS scratch for split walks (kWaveScratchBytes)
+    uint8_t* pool;            // the workgroup's walk pool in LDS (RT_SPH_POOL, sphere_pool_bytes)
     const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
     float* xstash;            // MIS: per-lane primary hit (p, din), SoA in LDS (rt_mis.hip)
 };
@@ -638,6 +639,306 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
     }
 }
 
+// ---------------------------------------------------------------------------
+// Workgroup walk pool (RT_SPH_POOL).  A wave's per-lane walks
+// take as long as its longest one (a lane walks ~38 entries, its wave ~103):
+// the lanes that finish early idle.  Here every lane's query sits in its own
+// LDS slot; once at most RT_SPH_POOL_T walks of a wave are left, the wave hands
+// them to the workgroup's pool (slot state + a bit in its `ready` mask) and
+// its idle lanes -- like those of every wave of the workgroup that has handed
+// over -- claim handed-over walks, of any wave and of either kind, and walk
+// them to the end.  The result goes back to the query's slot (and a bit in
+// the owner's `done` mask); every lane finally reads its own query back.
+// Packing the tails of 16 waves into few dense waves is the point: the
+// waiting waves issue nothing (s_sleep) and leave their SIMD to others.
+//
+// Exactness: a walk is the same sequence of entries and the same arithmetic
+// whichever lane runs it (the ray, running best and entry index travel
+// bit-exactly through LDS; a and the slab constants are recomputed from d
+// by the same code), so results are those of sphere_walk_lds.  tmin of a
+// pooled walk is implied by its kind: 0 for shadow (any-hit) walks
+// (raytrace.metal:79-85 leaves min_distance at 0) and 1e-3 for closest walks
+// (sampling.metal:154) -- the only two queries of the path.  The box tests
+// use tmin 0 for both (a superset of the entries: conservative).
+//
+// Liveness: a claimed walk always ends (entry indices only grow), a wave
+// never leaves the walk while it holds claimed walks, and a wave waiting for
+// its own handed-over walks claims them itself when nobody else has.
+#ifndef RT_SPH_POOL_T
+#define RT_SPH_POOL_T 16      // hand over once <= T walks of the wave are left
+#endif
+#ifndef RT_SPH_POOL_REFILL
+#define RT_SPH_POOL_REFILL 8  // idle lanes (beyond the last claim) that trigger another claim
+#endif
+
+typedef __attribute__((address_space(3))) float4 lds_f4_t;
+typedef __attribute__((address_space(3))) float lds_f32_t;
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) unsigned long long lds_u64_t;
+
+struct PoolView {
+    lds_f4_t* a;      // [NT] o, best
+    lds_f4_t* b;      // [NT] d, entry index (bits)
+    lds_u32_t* c;     // [NT] id + 1 | any-hit << 31
+    lds_u64_t* ready; // [NW] handed-over walks not claimed yet (bit = lane)
+    lds_u64_t* done;  // [NW] handed-over walks finished
+    lds_u32_t* sum;   // waves with ready walks (bit = wave)
+};
+
+template <uint32_t NT>
+__device__ __forceinline__ PoolView pool_view(uint8_t* base) {
+    typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
+    lds_u8_t* p = (lds_u8_t*)base;
+    PoolView v;
+    v.a = (lds_f4_t*)p;
+    v.b = (lds_f4_t*)(p + 16u * NT);
+    v.c = (lds_u32_t*)(p + 32u * NT);
+    v.ready = (lds_u64_t*)(p + 36u * NT);
+    v.done = (lds_u64_t*)(p + 36u * NT + 8u * (NT / 64u));
+    v.sum = (lds_u32_t*)(p + 36u * NT + 16u * (NT / 64u));
+    return v;
+}
+
+// Zero the masks (every thread of the workgroup calls it before the first
+// __syncthreads of the kernel).
+template <uint32_t NT>
+__device__ __forceinline__ void pool_init(uint8_t* base, uint32_t tid) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const PoolView v = pool_view<NT>(base);
+    if (tid < NT / 64u) {
+        v.ready[tid] = 0ull;
+        v.done[tid] = 0ull;
+    }
+    if (tid == 0) *v.sum = 0u;
+#endif
+}
+
+// Claim handed-over walks for the idle lanes (`idle`, wave-uniform).  Returns,
+// per lane, the claimed slot or 0xFFFFFFFF.  Own wave first (liveness), then
+// the waves the summary names.  Called by the whole wave (uniform control).
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t pool_claim(const PoolView& v, uint32_t wave, bool own_first,
+                                               unsigned long long idle) {
+    uint32_t got = 0xFFFFFFFFu;
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr uint32_t NW = NT / 64u;
+    uint32_t cand = __hip_atomic_load(v.sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    cand = wave_uniform(cand);
+    if (own_first) cand |= 1u << wave;
+    // rotate so the scan starts at this wave
+    cand = ((cand >> wave) | (cand << ((NW - wave) % NW))) & ((1u << NW) - 1u);
+    while (cand != 0u && idle != 0ull) {
+        const uint32_t k = (uint32_t)__builtin_ctz(cand);
+        cand &= cand - 1u;
+        const uint32_t w = (wave + k) % NW;
+        // take at most as many walks as there are idle lanes: the lowest bits
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        unsigned long long want = ~0ull;
+        {
+            unsigned long long r = __hip_atomic_load(&v.ready[w], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            r = ((unsigned long long)wave_uniform((uint32_t)(r >> 32)) << 32) | wave_uniform((uint32_t)r);
+            if (r == 0ull) continue;
+            want = r;
+            while ((uint32_t)__popcll(want) > n_idle) want &= ~(1ull << (63 - __builtin_clzll(want)));
+        }
+        unsigned long long old = 0ull;
+        if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+            old = __hip_atomic_fetch_and(&v.ready[w], ~want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = ((unsigned long long)wave_uniform((uint32_t)(old >> 32)) << 32) | wave_uniform((uint32_t)old);
+        unsigned long long cl = old & want;
+        if (old != 0ull && (old & ~want) == 0ull &&
+            __lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+            __hip_atomic_fetch_and(v.sum, ~(1u << w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // deal the claimed walks to idle lanes in order
+        while (cl != 0ull) {
+            const uint32_t s = (uint32_t)__builtin_ctzll(cl);
+            const uint32_t l = (uint32_t)__builtin_ctzll(idle);
+            cl &= cl - 1ull;
+            idle &= idle - 1ull;
+            got = (__lane_id() == l) ? w * 64u + s : got;
+        }
+    }
+#endif
+    return got;
+}
+
+template <bool ANY>
+__device__ __forceinline__ void sphere_walk_pool(const uint4* __restrict__ ent,
+                                                 const uint16_t* __restrict__ ids, uint32_t nN,
+                                                 uint32_t nT, uint8_t* pool_base, f3& o, f3& d,
+                                                 float& best, int& id) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr uint32_t NT = RT_SPH_BLOCK;
+    constexpr uint32_t kNone = 0xFFFFFFFFu, kClaimed = 0x10000u, kAnyBit = 0x20000u;
+#ifdef RT_TIMING_NO_SPH_WALK
+    return;
+#endif
+    const PoolView v = pool_view<NT>(pool_base);
+    // threadIdx.x through an opaque copy at each use: slot addresses hoisted
+    // out of the sample loop would hold VGPRs (and spill) for the whole launch
+    auto opaque_me = []() {
+        uint32_t t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+    uint32_t me = opaque_me();
+    const uint32_t wave = wave_uniform(me >> 6);
+    const uint32_t lane = __lane_id();
+    // this lane's query in its slot: read back at the end, whoever walked it
+    v.a[me] = make_float4(o.x, o.y, o.z, best);
+    v.b[me] = make_float4(d.x, d.y, d.z, 0.0f);
+    float a = dot(d, d);
+    RayBox rb = ray_box(o, d);
+    uint32_t idx = octant(d) * nN;
+    uint32_t end = idx + nN;
+    if (ANY && id >= 0) idx = end;
+    uint32_t cur = me | (ANY ? kAnyBit : 0u);   // slot of the walk this lane runs (+ kind bits)
+    float pb = 0.0f, pdisc = 0.0f;               // parked leaf idx - 1 while pdisc > 0
+    unsigned long long handed = 0ull;            // wave-uniform: walks this wave handed over
+    bool over = false;                           // wave-uniform: handed over (once per query)
+    const int n_exec = __popcll(__builtin_amdgcn_ballot_w64(true));
+    int refill_at = 0;                           // wave-uniform
+    uint32_t guard = 0;                          // wave-uniform: polls while waiting
+    for (;;) {
+        for (;;) {  // cheap steps
+            const bool adv = idx < end && !(pdisc > 0.0f);
+            if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
+            if (adv) {
+                const uint4 e = ent[idx];
+                if (e.w & 0x80000000u) {
+                    idx = lds_node_hit(e, rb, 0.0f, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
+                } else {  // sph_test up to the discriminant (shaders_old.metal:108-136)
+                    const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y), __uint_as_float(e.z)};
+                    const float bq = 2.0f * dot(oc, d);
+                    const float cc = dot(oc, oc) - __uint_as_float(e.w);
+                    const float disc = bq * bq - (4.0f * a) * cc;
+                    if (disc > 0.0f) {
+                        pb = bq;
+                        pdisc = disc;
+                    }
+                    idx = idx + 1;
+                }
+            }
+            const int parked = __popcll(__builtin_amdgcn_ballot_w64(pdisc > 0.0f));
+            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || pdisc > 0.0f));
+            if (RT_SPH_PARK_DEN * parked >= live) break;
+            if (!over ? live <= RT_SPH_POOL_T : n_exec - live >= refill_at) break;
+        }
+        if (__builtin_amdgcn_ballot_w64(pdisc > 0.0f) != 0) {  // roots of the parked leaves
+            if (pdisc > 0.0f) {
+                const bool any = (cur & kAnyBit) != 0u;
+                const float tmin = any ? 0.0f : 1e-3f;
+                const float sq = sqrtf(pdisc);
+                const float a2 = 2.0f * a;
+                float t = (-pb - sq) / a2;
+                if (!(t > tmin)) t = (-pb + sq) / a2;
+                if (any) {
+                    if (t > tmin && t < best) {
+                        id = 0;
+                        idx = end;
+                    }
+                } else if (t > tmin && t < 3.0e38f && t <= best) {
+                    const int s = (int)(nT + ids[idx - 1u]);
+                    if (t < best || s < id) {
+                        best = t;
+                        id = s;
+                    }
+                }
+                pdisc = 0.0f;
+            }
+        }
+        // finished walks: the result to the query's slot (claimed: + the owner's done bit)
+        const bool fin = cur != kNone && idx >= end;
+        if (fin) {
+            const uint32_t s = cur & 0xFFFFu;
+            ((lds_f32_t*)&v.a[s])[3] = best;
+            v.c[s] = (uint32_t)(id + 1);
+        }
+        if (__builtin_amdgcn_ballot_w64(fin && (cur & kClaimed)) != 0ull) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (fin && (cur & kClaimed))
+                __hip_atomic_fetch_or(&v.done[(cur & 0xFFFFu) >> 6], 1ull << (cur & 63u), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (fin) {
+            cur = kNone;
+            idx = end = 0u;
+        }
+        // hand over this wave's last walks (all of them are its own until now)
+        if (!over) {
+            const unsigned long long give = __builtin_amdgcn_ballot_w64(cur != kNone);
+            if (__popcll(give) <= RT_SPH_POOL_T) {
+                over = true;
+                handed = give;
+                if (give != 0ull) {
+                    if (cur != kNone) {
+                        me = cur & 0xFFFFu;  // (own walks only before the hand-over)
+                        ((lds_f32_t*)&v.a[me])[3] = best;
+                        ((lds_u32_t*)&v.b[me])[3] = idx;
+                        v.c[me] = (uint32_t)(id + 1) | ((cur & kAnyBit) ? 0x80000000u : 0u);
+                        cur = kNone;
+                        idx = end = 0u;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) {
+                        __hip_atomic_fetch_or(&v.ready[wave], give, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_or(v.sum, 1u << wave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+        }
+        if (!over) continue;
+        // idle lanes claim handed-over walks (this wave's first)
+        const unsigned long long idle = __builtin_amdgcn_ballot_w64(cur == kNone);
+        bool waiting = false;
+        if (idle != 0ull) {
+            const uint32_t got = pool_claim<NT>(v, wave, handed != 0ull, idle);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (got != kNone) {
+                const float4 qa = v.a[got], qb = v.b[got];
+                const uint32_t qc = v.c[got];
+                o = f3{qa.x, qa.y, qa.z};
+                best = qa.w;
+                d = f3{qb.x, qb.y, qb.z};
+                idx = __float_as_uint(qb.w);
+                id = (int)(qc & 0x7FFFFFFFu) - 1;
+                cur = got | kClaimed | ((qc >> 31) ? kAnyBit : 0u);
+                a = dot(d, d);
+                rb = ray_box(o, d);
+                end = (octant(d) + 1u) * nN;
+            }
+            refill_at = n_exec - __popcll(__builtin_amdgcn_ballot_w64(idx < end)) + RT_SPH_POOL_REFILL;
+        }
+        if (__builtin_amdgcn_ballot_w64(cur != kNone) == 0ull) {
+            // nothing to walk: done once every handed-over walk of this wave is back
+            unsigned long long dn = __hip_atomic_load(&v.done[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            dn = ((unsigned long long)wave_uniform((uint32_t)(dn >> 32)) << 32) | wave_uniform((uint32_t)dn);
+            if ((dn & handed) == handed) break;
+            waiting = true;
+        }
+        if (waiting) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++guard > (1u << 18)) {  // liveness guard (never expected): poison the result
+                best = __uint_as_float(0x7FC00000u);
+                break;
+            }
+        }
+    }
+    if (handed != 0ull && lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+        __hip_atomic_fetch_and(&v.done[wave], ~handed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    me = opaque_me();
+    const float4 qa = v.a[me], qb = v.b[me];
+    const uint32_t qc = v.c[me];
+    const float b0 = best;
+    o = f3{qa.x, qa.y, qa.z};
+    d = f3{qb.x, qb.y, qb.z};
+    best = (b0 != b0) ? b0 : qa.w;
+    id = (int)(qc & 0x7FFFFFFFu) - 1;
+#endif
+}
+
 template <bool PACKET>
 __device__ __forceinline__ bool sphere_any_lds(const uint4* ent, uint32_t nN, f3 o, f3 d,
                                                float tmin, float tmax) {
@@ -1077,8 +1378,10 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
 // With CULL (used for coherent camera rays) a pair is skipped when no lane's
 // box around its current candidate segment [o, o + d*best] touches the pair's
 // padded AABB: any hit that could still win has t < best and lies inside it.
+// o and d are references so that the pooled sphere walk (which hands them
+// back bit-identical) does not make the caller keep a second copy live.
 template <int GEO, bool SPH, bool CULL, int QT = 0>
-__device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, float tmin,
+__device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, float tmin,
                                            float* t_io) {
     float best = *t_io;
     int id = -1;
@@ -1151,6 +1454,8 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
     }
     if (SPH && GEO == kGeoSphLds && ((CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3))
         sphere_closest_lds<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
+    else if (SPH && GEO == kGeoSphLds && RT_SPH_POOL)
+        sphere_walk_pool<false>(sv.sent, sv.sid, sv.nN, sv.nT, sv.pool, o, d, best, id);
     else if (SPH && GEO == kGeoSphLds)
         sphere_walk_lds<false, RT_SPH_SPLIT != 0>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id,
                                                   sv.wscr);
@@ -1166,7 +1471,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3 o, f3 d, floa
 // pair whose padded AABB no lane's segment box touches cannot be hit by any
 // lane of the wave and is skipped as a whole.
 template <int GEO, bool SPH, bool PACKET>
-__device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float tmin, float tmax,
+__device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float tmin, float tmax,
                                         f3 seg_lo, f3 seg_hi) {
     if (GEO == kGeoPairClu) {
         float tm = tmax;
@@ -1219,6 +1524,12 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3 o, f3 d, float t
         }
     }
     if (SPH && GEO == kGeoSphLds && PACKET) return sphere_any_lds<true>(sv.sent, sv.nN, o, d, tmin, tmax);
+    if (SPH && GEO == kGeoSphLds && RT_SPH_POOL) {
+        float tm = tmax;
+        int id = -1;
+        sphere_walk_pool<true>(sv.sent, sv.sid, sv.nN, sv.nT, sv.pool, o, d, tm, id);
+        return id >= 0;
+    }
     if (SPH && GEO == kGeoSphLds) {
         float tm = tmax;
         int id = -1;
