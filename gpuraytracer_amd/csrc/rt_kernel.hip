@@ -387,8 +387,18 @@ __host__ __device__ constexpr bool halton_tables_on(int geo, bool small, uint32_
 // order n — the same sequence of fp32 additions as one lane per pixel.
 // Workgroup size: 1024 threads (4x4 waves) when the sphere BVH is staged in
 // LDS, so one ~72 KB copy serves 16 waves; 256 (2x2 waves) otherwise.
-constexpr uint32_t block_threads(int geo) { return geo == kGeoSphLds ? RT_SPH_BLOCK : kBlockThreads; }
-constexpr uint32_t waves_per_row(int geo) { return geo == kGeoSphLds ? 4u : 2u; }
+#ifndef RT_CLU_BLOCK
+#define RT_CLU_BLOCK 256  // threads per workgroup of the box-cluster (Cornell) kernel
+#endif
+constexpr uint32_t block_threads(int geo) {
+    return geo == kGeoSphLds ? RT_SPH_BLOCK : (geo == kGeoPairClu ? RT_CLU_BLOCK : kBlockThreads);
+}
+#ifndef RT_SPH_WR
+#define RT_SPH_WR (RT_SPH_BLOCK >= 256 ? 4u : RT_SPH_BLOCK / 64u)  // waves per workgroup row
+#endif
+constexpr uint32_t waves_per_row(int geo) {
+    return geo == kGeoSphLds ? (uint32_t)(RT_SPH_WR) : (block_threads(geo) >= 128 ? 2u : 1u);
+}
 constexpr uint32_t waves_per_col(int geo) { return block_threads(geo) / 64u / waves_per_row(geo); }
 
 template <int B, int GEO, bool SPH, bool SMALL, int L = 1>

@@ -43,13 +43,23 @@ constexpr uint32_t kWaveScratchBytes = 576;
 inline constexpr size_t sphere_pool_bytes(uint32_t block_threads) {
     return (size_t)block_threads * 36u + (size_t)(block_threads / 64u) * 16u + 16u;
 }
-// Layouts of the compact sphere BVH (rt_scene.cpp build_sphere_lds): 2 --
-// octants (+,+,+) and (-,-,-), staged in LDS -- or 8, one per direction
-// octant, too big for LDS and read from global memory (L2) instead.
+// Layouts of the compact sphere BVH (rt_scene.cpp build_sphere_lds): 8, one
+// per direction octant (256 KB at 1000 spheres), read from global memory
+// (L2-resident) with near/far boxes and 256-thread workgroups (round 3:
+// config 4 194 -> 161 ms) -- or 2, octants (+,+,+) and (-,-,-),
+// staged in LDS by 1024-thread workgroups (the round-2 kernel, opt-in).
 #ifndef RT_SPH_LAYOUTS
-#define RT_SPH_LAYOUTS 2
+#define RT_SPH_LAYOUTS 8
 #endif
 static_assert(!RT_SPH_POOL || RT_SPH_LAYOUTS == 8, "the walk pool takes the LDS of the 2-layout tree");
+// Near/far boxes (rt_scene.cpp build_sphere_lds): with one layout per direction
+// octant, each layout stores a box's entry planes in the lo slots, and the
+// per-lane walks (whose layout is their ray's octant) test the slab with
+// 4 min/max instead of 10 (rt_trace.hpp lds_node_hit_nf).
+#ifndef RT_SPH_NEARFAR
+#define RT_SPH_NEARFAR (RT_SPH_LAYOUTS == 8 ? 1 : 0)
+#endif
+static_assert(!RT_SPH_NEARFAR || RT_SPH_LAYOUTS == 8, "near/far boxes need one layout per octant");
 // dynamic LDS of the LDS-sphere kernel: pair records, both layouts of the
 // compact BVH, then the wave scratch (RT_SPH_SPLIT) or the entry ids
 inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t block_threads) {
@@ -60,8 +70,13 @@ inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t b
            (RT_SPH_SPLIT ? (size_t)(block_threads / 64u) * kWaveScratchBytes
                          : ((2u * (size_t)n_entries * 2u + 3u) & ~(size_t)3u));
 }
+// threads per workgroup of the sphere kernel: 1024 (4x4 waves, two per CU)
+// when one LDS copy of the 2-layout tree serves 16 waves; ONE wave with the
+// tree in L2 -- a workgroup's wave slots and LDS stay taken until its slowest
+// wave ends, and the sphere walks make wave times differ a lot (config 4:
+// 1024 threads 186.1 ms, 512 177.9, 256 162.1, 128 160.5, 64 158.4)
 #ifndef RT_SPH_BLOCK
-#define RT_SPH_BLOCK 1024  // threads per workgroup of the LDS-sphere-BVH kernel (768: 4x3 waves)
+#define RT_SPH_BLOCK (RT_SPH_LAYOUTS == 8 ? 64 : 1024)
 #endif
 constexpr uint32_t kSphBlockThreads = RT_SPH_BLOCK;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)

@@ -458,6 +458,10 @@ static void build_sphere_lds(CompiledScene* out) {
                     if (!isfinite(n.lo[a]) || !isfinite(n.hi[a])) return;
                     h[a] = half_dir(n.lo[a], -1);
                     h[3 + a] = half_dir(n.hi[a], +1);
+                    // RT_SPH_NEARFAR: in the layout of octant `oct` the box plane a ray
+                    // of that octant enters through (hi when component a is negative)
+                    // takes the lo slot, so the walk's slab test needs no min/max pairs
+                    if (RT_SPH_NEARFAR && ((oct >> a) & 1)) std::swap(h[a], h[3 + a]);
                 }
                 if (n.escape > nn) return;
                 const uint32_t w[4] = {h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,

@@ -378,6 +378,22 @@ __device__ __forceinline__ bool lds_node_hit(const uint4& e, const RayBox& rb, f
     return node_hit(n0, n1, rb, tmin, tmax);
 }
 
+// Slab test of a near/far entry (RT_SPH_NEARFAR): the lo slots hold the planes
+// the ray enters through, which holds for every ray whose direction octant is
+// the layout's.  Equal to lds_node_hit for such rays: fma(p, invd, -oinv) is
+// monotone in p and sign(invd) orders the two planes of each axis, so the
+// min/max pairs of node_hit select exactly these values.
+__device__ __forceinline__ bool lds_node_hit_nf(const uint4& e, const RayBox& rb, float tmin,
+                                                float tmax) {
+    const float nx = fmaf(h2f(e.x & 0xFFFFu), rb.invd.x, -rb.oinv.x);
+    const float ny = fmaf(h2f(e.x >> 16), rb.invd.y, -rb.oinv.y);
+    const float nz = fmaf(h2f(e.y & 0xFFFFu), rb.invd.z, -rb.oinv.z);
+    const float fx = fmaf(h2f(e.y >> 16), rb.invd.x, -rb.oinv.x);
+    const float fy = fmaf(h2f(e.z & 0xFFFFu), rb.invd.y, -rb.oinv.y);
+    const float fz = fmaf(h2f(e.z >> 16), rb.invd.z, -rb.oinv.z);
+    return vmax3(nx, ny, vmax(nz, tmin)) <= vmin3(fx, fy, vmin(fz, tmax));
+}
+
 template <bool PACKET>
 __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint16_t* ids,
                                                    uint32_t nN, uint32_t nT, f3 o, f3 d,
@@ -503,7 +519,9 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             if (adv) {
                 const uint4 e = ent[idx];
                 if (e.w & 0x80000000u) {
-                    idx = lds_node_hit(e, rb, tmin, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
+                    const bool h = RT_SPH_NEARFAR && !SPLIT ? lds_node_hit_nf(e, rb, tmin, best)
+                                                            : lds_node_hit(e, rb, tmin, best);
+                    idx = h ? idx + 1 : (e.w & 0x7FFFFFFFu);
                 } else {  // sph_test up to the discriminant (shaders_old.metal:108-136)
                     const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y),
                                          __uint_as_float(e.z)};

@@ -178,15 +178,17 @@ def test_rgba8_device_output_progressive():
 
 
 C4_KERNEL = "rt::path_trace_kernel<3, 7, true, true, 16>"  # what bench.py --scene spheres times
+C4_BLOCK = 64                  # one wave of 2x2 pixels per workgroup (rt_kernel.hpp RT_SPH_BLOCK)
+C4_GRID = (1920 // 2, 1080 // 2)
 
 
 def test_c4_timed_launch_1080p_256spp_bands_vs_oracle():
     """Config 4 exactly as the bench times it: the whole 1920x1080 frame of the
     1000-sphere scene at 256 spp in ONE launch (16 lanes per pixel, 16 rounds
-    per lane, 1024-thread workgroups with the compact BVH in LDS, grid
-    240x135).  Three 4-row bands of that frame (top, middle, lower third) are
-    compared with the brute-force oracle bit for bit (5.9 M samples on the
-    host); the whole frame is finite with alpha 1."""
+    per lane, C4_BLOCK-thread workgroups walking the compact 8-layout BVH in
+    L2, grid C4_GRID).  Three 4-row bands of that frame (top, middle, lower
+    third) are compared with the brute-force oracle bit for bit (5.9 M
+    samples on the host); the whole frame is finite with alpha 1."""
     W, H = 1920, 1080
     s = Scene.random_spheres(W, H, 1000, seed=42)
     sd = seed_splitmix(W, H)
@@ -194,8 +196,8 @@ def test_c4_timed_launch_1080p_256spp_bands_vs_oracle():
         frame = r.render(RenderParams(spp=256, bounces=3))
         info = r.last_launch()
     assert info["kernel"] == C4_KERNEL, info
-    assert info["lanes_per_pixel"] == 16 and info["block_threads"] == 1024, info
-    assert (info["grid_x"], info["grid_y"]) == (240, 135), info
+    assert info["lanes_per_pixel"] == 16 and info["block_threads"] == C4_BLOCK, info
+    assert (info["grid_x"], info["grid_y"]) == C4_GRID, info
     assert info["lds_bytes"] == s.describe()["sphere_bvh_lds_bytes"], info
     assert np.isfinite(frame).all() and np.all(frame[..., 3] == 1.0)
     for start in (100, 540, 900):

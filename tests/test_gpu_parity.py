@@ -125,8 +125,9 @@ def test_duplicate_spheres_tie_to_lower_id():
 
 @pytest.mark.parametrize("layout", ["auto", "pairs"])
 def test_sphere_bvh_lds_and_global_walks_bit_exact(layout, monkeypatch):
-    """auto: the compact fp16 sphere BVH in LDS (1024-thread workgroups);
-    pairs: the 8-layout BVH read from global memory.  Both are the oracle."""
+    """auto: the compact fp16 sphere BVH (8 octant layouts, near/far boxes,
+    per-lane walks); pairs: the 32-B-node BVH read with scalar loads in the
+    pair-record kernel.  Both are the oracle."""
     if layout != "auto":
         monkeypatch.setenv("RTPT_SCENE_MEM", layout)
     s = Scene.random_spheres(40, 24, 700, seed=13)
