@@ -110,7 +110,7 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         *nt = h.t;
         return true;
     }
-    if (!any_hit<GEO, SPH, (b == 0 && RT_SPH_PACKET) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
+    if (!any_hit<GEO, SPH, (b == 0 && (SPH ? RT_SPH_PACKET : 1)) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + contrib;                           // :87-89
     if (b + 1 < B) {
         s.d = d2;
@@ -390,8 +390,12 @@ __host__ __device__ constexpr bool halton_tables_on(int geo, bool small, uint32_
 #ifndef RT_CLU_BLOCK
 #define RT_CLU_BLOCK 256  // threads per workgroup of the box-cluster (Cornell) kernel
 #endif
+#ifndef RT_TRI_BLOCK
+#define RT_TRI_BLOCK 256  // threads per workgroup of the triangle-BVH kernel
+#endif
 constexpr uint32_t block_threads(int geo) {
-    return geo == kGeoSphLds ? RT_SPH_BLOCK : (geo == kGeoPairClu ? RT_CLU_BLOCK : kBlockThreads);
+    return geo == kGeoSphLds ? RT_SPH_BLOCK
+                             : (geo == kGeoPairClu ? RT_CLU_BLOCK : (geo == kGeoTriBvh ? RT_TRI_BLOCK : kBlockThreads));
 }
 #ifndef RT_SPH_WR
 #define RT_SPH_WR (RT_SPH_BLOCK >= 256 ? 4u : RT_SPH_BLOCK / 64u)  // waves per workgroup row

@@ -247,7 +247,11 @@ __device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, con
 }
 
 #ifndef RT_SPH_PACKET
-#define RT_SPH_PACKET 1  // 1: packet walks for camera and bounce-0 shadow rays; 2: + all shadow rays; 3: all
+// sphere scenes: 1: wave-packet walks for camera and bounce-0 shadow rays;
+// 2: + all shadow rays; 3: all; 0 (round 3): per-lane walks for every ray --
+// with the near/far L2 tree and one-wave workgroups 155.8 vs 158.4 ms on
+// config 4.  (Triangle-BVH scenes keep packets for bounce-0 shadow rays.)
+#define RT_SPH_PACKET 0
 #endif
 
 // BVH layout of a ray direction: bit a set when component a is negative.
@@ -459,7 +463,7 @@ __device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint1
 // entries visited by a split walk can only add candidates that are real hits
 // in (tmin, tmax), so the minimum is the brute-force one.
 #ifndef RT_SPH_PARK_DEN
-#define RT_SPH_PARK_DEN 4  // the parked roots run once they are >= 1/DEN of the live lanes
+#define RT_SPH_PARK_DEN 2  // the parked roots run once they are >= 1/DEN of the live lanes (L2 tree: 2 157.3 ms, 4 158.4, 6 161.1)
 #endif
 #ifndef RT_SPH_SPLIT_CLOSEST_ONLY
 #define RT_SPH_SPLIT_CLOSEST_ONLY 0  // 1: shadow (any-hit) walks are not split
