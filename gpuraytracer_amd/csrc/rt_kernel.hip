@@ -197,6 +197,9 @@ __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv
 #ifndef RT_DPP_SUM
 #define RT_DPP_SUM 1
 #endif
+#ifndef RT_DPP_SUM_SPH
+#define RT_DPP_SUM_SPH 0  // the sphere kernel: 2,715 vs 2,724 Msamples/s with the round-2 LDS tree
+#endif
 template <int k>
 __device__ __forceinline__ float row_shl(float v) {
     if constexpr (k == 0) {
@@ -582,7 +585,7 @@ void path_trace_kernel(KParams P) {
         }
         if (L == 1) {
             lum = lum + s.acc;                                   // :103
-        } else if (RT_DPP_SUM && L <= 16 && !SPH) {  // (the sphere kernel keeps ds_bpermute:
+        } else if (RT_DPP_SUM && L <= 16 && (!SPH || RT_DPP_SUM_SPH)) {  // (the sphere kernel keeps ds_bpermute:
                                                        //  the DPP form spills 3 more VGPRs there)
             // a pixel's L lanes are consecutive lanes of one 16-lane DPP row
             // (L = 4: groups at 0, 4, 8, 12; L = 16: the whole row), so its
