@@ -645,8 +645,8 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
                                            std::min(lds_pairs, lds_single) > rt::kMaxLdsBytes)));
         if (need_bvh) {
             const size_t nn = 2 * (size_t)nT - 1;
-            // 8 layouts of 32-B nodes, then 2 compact layouts of 16-B entries (rt_lbvh.hip)
-            if ((e = hipMalloc((void**)&c->d_tri_nodes, (8 * nn * 2 + RT_TRI_COMPACT_LAYOUTS * nn) * sizeof(float4))) != hipSuccess ||
+            // 8 layouts of 32-B nodes, then 8 compact layouts of 16-B entries (rt_lbvh.hip)
+            if ((e = hipMalloc((void**)&c->d_tri_nodes, (8 * nn * 2 + rt::kTriCompactLayouts * nn) * sizeof(float4))) != hipSuccess ||
                 (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
                 (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
                 status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;
@@ -764,11 +764,13 @@ int rt_render_gather(rt_ctx* c, const rt_render_params* p, void* frame, void* hi
 
 int rt_comm_info(const rt_ctx* c, int32_t* count, int32_t* rank) {
     if (!c || !count || !rank) return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
-    if (!c->comm) return RT_ERR_STATE;
+    rt_ctx* m = const_cast<rt_ctx*>(c);  // the error message slot only
+    if (!c->comm) return fail(m, RT_ERR_STATE, "rt_comm_info: no communicator (rt_comm_init first)");
     int n = 0, r = 0;
     ncclResult_t res = ncclCommCount(c->comm, &n);
-    if (res == ncclSuccess) res = ncclCommUserRank(c->comm, &r);
-    if (res != ncclSuccess) return RT_ERR_COMM;
+    if (res != ncclSuccess) return nccl_fail(m, "ncclCommCount", res);
+    res = ncclCommUserRank(c->comm, &r);
+    if (res != ncclSuccess) return nccl_fail(m, "ncclCommUserRank", res);
     *count = n;
     *rank = r;
     return RT_OK;
@@ -863,9 +865,8 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
                      std::min(lds, lds_single) > rt::kMaxLdsBytes;
     info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
     {
-        const size_t b = rt::sphere_lds_bytes(lds, s.sph_lds_entries, rt::kSphBlockThreads);
-        info->sphere_bvh_lds_bytes =
-            (!s.sph_lds.empty() && lds <= rt::kMaxLdsBytes && b <= rt::kSphLdsMaxBytes) ? (uint32_t)b : 0u;
+        info->sphere_kernel_lds_bytes =
+            (!s.sph_lds.empty() && lds <= rt::kSphPairLdsMaxBytes) ? (uint32_t)lds : 0u;
     }
     // box clusters are staged after the pairs in triangle-only scenes
     const size_t lds_clu =

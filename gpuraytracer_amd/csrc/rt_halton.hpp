@@ -78,9 +78,6 @@ constexpr int kSmallIndexBits = 21;           // base-2 bit-reversal width
 static_assert(kSmallIndexMax <= (1u << kSmallIndexBits), "float digit steps need x < 2^21");
 template <uint32_t D>
 __device__ __forceinline__ float halton_small(uint32_t i) {
-#ifdef RT_TIMING_NO_HALTON  // timing-only experiment (share of the Halton digits), NOT exact
-    return (float)((i * (2654435761u + 2u * D)) >> 8) * (1.0f / 16777216.0f);
-#endif
     constexpr uint32_t b = kPrimes[D];
     if constexpr (b == 2) {
         return (float)(__builtin_bitreverse32(i) >> (32 - kSmallIndexBits)) *
@@ -187,10 +184,8 @@ __device__ __forceinline__ float halton_tab(uint32_t i, const float* tab) {
 // filling them.
 template <uint32_t D, bool SMALL, bool TAB = false>
 __device__ __forceinline__ float halton_dim(uint32_t i, const float* tab = nullptr) {
-#ifndef RT_TIMING_NO_HALTON
     if constexpr (TAB && SMALL && kTabDigits[D] > 0)
         if (tab != nullptr) return halton_tab<D>(i, tab);
-#endif
     if (SMALL) return halton_small<D>(i);
     return halton<D>(i);
 }

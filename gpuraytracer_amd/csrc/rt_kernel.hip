@@ -1,16 +1,20 @@
 // rt_kernel.hip — gfx950 path-tracing kernel (the hot path) and its launcher.
 //
 // Rebuilds `kernel pathTrace` (RTrace/raytrace.metal:11-111) for CDNA4:
-//   * the scene's intersection records (triangles 48 B, spheres 16 B) are
-//     staged into LDS once per workgroup and read with wave-uniform addresses
-//     (LDS broadcast); shading records are fetched from global only on a hit;
-//   * one lane per pixel, a wave64 covers an 8x8 pixel tile (the reference's
-//     8x8 threadgroup, renderer.swift:139), a 256-thread workgroup 16x16;
+//   * the scene's intersection records (shared-edge triangle pairs, box
+//     clusters) and the Halton low-digit tables are staged into LDS once per
+//     workgroup; the sphere and triangle BVHs are read from global memory
+//     (L2-resident); shading records are fetched from global only on a hit;
+//   * L = 4 or 16 lanes per pixel: a wave traces 64/L pixels (a 4x4 or 2x2
+//     tile, or one row of interleaved rows), lane `sub` traces samples
+//     n = r*L + sub, and the colours are summed at the pixel's leader in
+//     sample order (DPP row shifts or ds_bpermute) -- the additions of one
+//     lane per pixel, so the result is unchanged;
 //   * the bounce loop is unrolled at compile time (template B) so every Halton
-//     dimension, hence every base, is a constant: `i % b` / `i / b` become
-//     magic-number multiplies (exact for u32, so the values are unchanged);
+//     dimension, hence every base, is a constant: the digit steps run in float
+//     (floor(x*c), fma(q, -b, x): exact for indices < 3^13, rt_halton.hpp);
 //   * camera constants are precomputed on the host once (same contract ops);
-//   * the per-pixel result is one coalesced float4 (or half4) store.
+//   * the per-pixel result is one coalesced float4 / half4 / uchar4 store.
 // Arithmetic follows the contract of rt_math.h / DESIGN.md §3 so the result is
 // bit-identical to the CPU oracle.
 #include <hip/hip_runtime.h>
@@ -100,9 +104,7 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
     }
     if (FUSE && b + 1 < B) {
-        const FusedHit h = GEO == kGeoPairClu
-                               ? fused_cluster_query(sv, p, L, dist - 1e-3f, d2)
-                               : fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
+        const FusedHit h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
         if (!h.occluded) s.acc = s.acc + contrib;          // :79-89
         s.d = d2;
         s.o = p;                                           // :99-100
@@ -110,7 +112,8 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         *nt = h.t;
         return true;
     }
-    if (!any_hit<GEO, SPH, (b == 0 && (SPH ? RT_SPH_PACKET : 1)) || RT_SPH_PACKET >= 2>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
+    // bounce-0 shadow rays of the triangle BVH walk as wave packets
+    if (!any_hit<GEO, SPH, b == 0 && !SPH>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + contrib;                           // :87-89
     if (b + 1 < B) {
         s.d = d2;
@@ -175,15 +178,13 @@ struct FusedChain<B, B, GEO, SMALL> {
                                                float) {}
 };
 
-#ifndef RT_FUSED
-#define RT_FUSED 1
-#endif
-#ifndef RT_FUSED_CLU
-#define RT_FUSED_CLU 0  // 1: fused_cluster_query (measured 5 % slower on Cornell 1080p)
-#endif
+// The pair layouts (triangles only) fuse the shadow query of bounce b with the
+// closest hit of bounce b + 1 (fused_shadow_closest).  The box-cluster kernel
+// does not: its fused candidate rounds measured 5 % slower on Cornell 1080p
+// (DESIGN.md §5).
 template <int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv, PathState& s) {
-    if (RT_FUSED && (geo_pairs(GEO) || (RT_FUSED_CLU && GEO == kGeoPairClu)) && !SPH && B > 1) {
+    if (geo_pairs(GEO) && !SPH && B > 1) {
         float t = 1000.0f;                                  // sampling.metal:155
         const int id = closest_hit<GEO, false, true, 0>(sv, s.o, s.d, 0.001f, &t);
         if (id >= 0) FusedChain<0, B, GEO, SMALL>::run(P, sv, s, id, t);
@@ -193,13 +194,9 @@ __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv
 }
 
 // In-order sum of the L colours of a pixel's lanes at its group leader, with
-// DPP row shifts (row_shl:k: lane i reads lane i + k of its 16-lane row).
-#ifndef RT_DPP_SUM
-#define RT_DPP_SUM 1
-#endif
-#ifndef RT_DPP_SUM_SPH
-#define RT_DPP_SUM_SPH 0  // the sphere kernel: 2,715 vs 2,724 Msamples/s with the round-2 LDS tree
-#endif
+// DPP row shifts (row_shl:k: lane i reads lane i + k of its 16-lane row).  The
+// sphere kernel keeps ds_bpermute shuffles (its DPP form spilled 3 more VGPRs:
+// 2,715 vs 2,724 Msamples/s).
 template <int k>
 __device__ __forceinline__ float row_shl(float v) {
     if constexpr (k == 0) {
@@ -364,12 +361,8 @@ size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 
 }  // namespace
 
-#ifndef RT_MIN_WAVES_PER_EU
-#define RT_MIN_WAVES_PER_EU 8  // 8 waves/SIMD (<= 64 VGPRs): +4.5% measured over 7
-#endif
-#ifndef RT_MIN_WAVES_PER_EU_SPH
-#define RT_MIN_WAVES_PER_EU_SPH 8
-#endif
+constexpr int kMinWavesPerEu = 8;     // 8 waves/SIMD (<= 64 VGPRs): +4.5% measured over 7
+constexpr int kMinWavesPerEuSph = 8;  // sphere kernel: 7 / 6 waves 162.2 / 176.3 ms vs 154.3
 constexpr uint32_t kHaltonTabMinRounds = 8;  // samples per lane below which no tables
 // Whether a launch fills the LDS low-digit Halton tables: box-cluster kernel,
 // fixed-digit indices, and every lane tracing enough samples to amortise the
@@ -378,41 +371,27 @@ constexpr uint32_t kHaltonTabMinRounds = 8;  // samples per lane below which no 
 __host__ __device__ constexpr bool halton_tables_on(int geo, bool small, uint32_t spp, uint32_t L) {
     return geo == kGeoPairClu && small && (spp + L - 1) / L >= kHaltonTabMinRounds;
 }
-#ifndef RT_MIN_WAVES_PER_EU_CLU
 // box-cluster kernel: 7 waves/SIMD runs as fast as 8 and spills 6 VGPRs
 // instead of 30 (HBM traffic 146 MB instead of 19 GB per 1080p launch)
-#define RT_MIN_WAVES_PER_EU_CLU 7
-#endif
+constexpr int kMinWavesPerEuClu = 7;
 // L lanes per pixel (1, 4 or 16: more lanes when the launch has few pixels,
 // e.g. one GPU's share of a multi-GPU frame): lane `sub` of a pixel's
 // group traces samples n = r*L + sub of round r, and after every round the L
 // colours are shuffled within the wave and added to the pixel's sum in sample
 // order n — the same sequence of fp32 additions as one lane per pixel.
-// Workgroup size: 1024 threads (4x4 waves) when the sphere BVH is staged in
-// LDS, so one ~72 KB copy serves 16 waves; 256 (2x2 waves) otherwise.
-#ifndef RT_CLU_BLOCK
-#define RT_CLU_BLOCK 256  // threads per workgroup of the box-cluster (Cornell) kernel
-#endif
-#ifndef RT_TRI_BLOCK
-#define RT_TRI_BLOCK 256  // threads per workgroup of the triangle-BVH kernel
-#endif
-constexpr uint32_t block_threads(int geo) {
-    return geo == kGeoSphLds ? RT_SPH_BLOCK
-                             : (geo == kGeoPairClu ? RT_CLU_BLOCK : (geo == kGeoTriBvh ? RT_TRI_BLOCK : kBlockThreads));
-}
-#ifndef RT_SPH_WR
-#define RT_SPH_WR (RT_SPH_BLOCK >= 256 ? 4u : RT_SPH_BLOCK / 64u)  // waves per workgroup row
-#endif
-constexpr uint32_t waves_per_row(int geo) {
-    return geo == kGeoSphLds ? (uint32_t)(RT_SPH_WR) : (block_threads(geo) >= 128 ? 2u : 1u);
-}
+// Workgroup size: one wave for the sphere kernel (rt_kernel.hpp
+// kSphBlockThreads), 256 threads (2x2 waves) otherwise -- the box-cluster
+// kernel at 128 / 64 / 512 threads ran 40.1 / 68.9 / 27.8 ms vs 26.2 (its 22 KB
+// of Halton tables per workgroup then cap the waves per CU), the
+// triangle-BVH kernel at 64 / 128 threads 204.3 / 192.1 ms vs 180.7.
+constexpr uint32_t block_threads(int geo) { return geo == kGeoSphLds ? kSphBlockThreads : kBlockThreads; }
+constexpr uint32_t waves_per_row(int geo) { return block_threads(geo) >= 128 ? 2u : 1u; }
 constexpr uint32_t waves_per_col(int geo) { return block_threads(geo) / 64u / waves_per_row(geo); }
 
 template <int B, int GEO, bool SPH, bool SMALL, int L = 1>
 __global__ __launch_bounds__(block_threads(GEO),
-                             SPH ? RT_MIN_WAVES_PER_EU_SPH
-                                 : (GEO == kGeoPairClu ? RT_MIN_WAVES_PER_EU_CLU
-                                                       : RT_MIN_WAVES_PER_EU))
+                             SPH ? kMinWavesPerEuSph
+                                 : (GEO == kGeoPairClu ? kMinWavesPerEuClu : kMinWavesPerEu))
 void path_trace_kernel(KParams P) {
     constexpr uint32_t NT = block_threads(GEO), WR = waves_per_row(GEO), WC = waves_per_col(GEO);
     extern __shared__ float4 lds[];
@@ -429,30 +408,9 @@ void path_trace_kernel(KParams P) {
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
-        if (GEO == kGeoSphLds && RT_SPH_LAYOUTS == 8) {  // 8 compact layouts: global (L2)
+        if (GEO == kGeoSphLds) {  // the compact sphere BVH (8 layouts) stays in global memory (L2)
             sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
             sv.sid = P.sph_lds_id;
-            // the walk pool after the pair records (RT_SPH_POOL)
-            sv.pool = reinterpret_cast<uint8_t*>(lds + ng4);
-            if (RT_SPH_POOL) pool_init<NT>(sv.pool, threadIdx.x);
-        } else if (GEO == kGeoSphLds) {  // compact sphere BVH (2 layouts) after the pairs
-            const uint32_t ne = 2u * P.nE;
-            const uint4* es = reinterpret_cast<const uint4*>(P.sph_lds);
-            uint4* ed = reinterpret_cast<uint4*>(lds + ng4);
-            for (uint32_t k = threadIdx.x; k < ne; k += NT) ed[k] = es[k];
-            sv.sent = ed;
-#if RT_SPH_SPLIT
-            // then one scratch per wave for the split walks; the entry ids
-            // (read only for a root that wins) stay in global memory
-            sv.wscr = reinterpret_cast<uint8_t*>(lds + ng4 + ne) +
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * kWaveScratchBytes;
-            sv.sid = P.sph_lds_id;
-#else
-            const uint32_t* is = reinterpret_cast<const uint32_t*>(P.sph_lds_id);
-            uint32_t* id = reinterpret_cast<uint32_t*>(lds + ng4 + ne);
-            for (uint32_t k = threadIdx.x; k < (ne + 1) / 2; k += NT) id[k] = is[k];
-            sv.sid = reinterpret_cast<const uint16_t*>(id);
-#endif
         }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
@@ -493,12 +451,9 @@ void path_trace_kernel(KParams P) {
     // still interleave over the XCDs, which keeps the cheap and the expensive
     // image regions evenly spread (contiguous bands per XCD ran 7 % slower).
     // Speed only: every tile is rendered exactly once.
-#ifndef RT_XCD_RUN
-#define RT_XCD_RUN 4  // 0: plain dispatch order
-#endif
     uint32_t bx, by;
     {
-        constexpr uint32_t kXcdRun = RT_XCD_RUN;
+        constexpr uint32_t kXcdRun = 4;  // runs of 0 (plain order) / 16: 158.9 / 157.6 vs 158.4 ms on config 4
         const uint32_t n = gridDim.x * gridDim.y, full = n / (8u * kXcdRun + (kXcdRun == 0)) * (8u * kXcdRun);
         const uint32_t p = blockIdx.y * gridDim.x + blockIdx.x;
         uint32_t t = p;
@@ -585,8 +540,7 @@ void path_trace_kernel(KParams P) {
         }
         if (L == 1) {
             lum = lum + s.acc;                                   // :103
-        } else if (RT_DPP_SUM && L <= 16 && (!SPH || RT_DPP_SUM_SPH)) {  // (the sphere kernel keeps ds_bpermute:
-                                                       //  the DPP form spills 3 more VGPRs there)
+        } else if (L <= 16 && !SPH) {
             // a pixel's L lanes are consecutive lanes of one 16-lane DPP row
             // (L = 4: groups at 0, 4, 8, 12; L = 16: the whole row), so its
             // leader reads sample r*L + k from lane +k with a row shift fused
@@ -643,7 +597,7 @@ void path_trace_kernel(KParams P) {
 }
 
 template <int B, bool SPH, bool SMALL>
-__global__ __launch_bounds__(kBlockThreads, RT_MIN_WAVES_PER_EU) void path_trace_sorted_kernel(
+__global__ __launch_bounds__(kBlockThreads, kMinWavesPerEu) void path_trace_sorted_kernel(
     KParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
@@ -728,26 +682,28 @@ __global__ void fill_seeds_kernel(uint32_t* seeds, uint64_t key, uint64_t n) {
 // device-to-device 2D copy enqueued on the null stream was measured to start
 // before the kernels enqueued ahead of it had finished (it read the gather
 // buffer's previous contents), and the kernel is one launch whatever N.
+// Frames taller than the grid's y extent walk their rows with a grid stride.
 template <typename U>
 __global__ void place_tiles_kernel(const U* __restrict__ gathered, U* __restrict__ frame, uint32_t row_u,
                                    size_t tile_u, uint32_t H, uint32_t N) {
-    const uint32_t y = blockIdx.y;
-    const uint32_t k = y % N, j = y / N;
-    const U* src = gathered + k * tile_u + (size_t)j * row_u;
-    U* dst = frame + (size_t)y * row_u;
-    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < row_u; u += gridDim.x * blockDim.x)
-        dst[u] = src[u];
+    for (uint32_t y = blockIdx.y; y < H; y += gridDim.y) {
+        const uint32_t k = y % N, j = y / N;
+        const U* src = gathered + k * tile_u + (size_t)j * row_u;
+        U* dst = frame + (size_t)y * row_u;
+        for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < row_u; u += gridDim.x * blockDim.x)
+            dst[u] = src[u];
+    }
 }
 
 hipError_t launch_place_tiles(const void* gathered, void* frame, size_t row_bytes, size_t tile_bytes,
                               uint32_t H, uint32_t N, hipStream_t stream) {
     if (H == 0 || N == 0 || row_bytes == 0) return hipSuccess;
-    if (row_bytes % 4 || tile_bytes % 4 || H > 65535u) return hipErrorInvalidValue;  // grid.y limit
+    if (row_bytes % 4 || tile_bytes % 4) return hipErrorInvalidValue;
     const bool wide = row_bytes % 16 == 0 && tile_bytes % 16 == 0 &&
                       reinterpret_cast<uintptr_t>(gathered) % 16 == 0 && reinterpret_cast<uintptr_t>(frame) % 16 == 0;
     const size_t unit = wide ? 16 : 4;
     const uint32_t row_u = (uint32_t)(row_bytes / unit);
-    const dim3 grid((row_u + 255u) / 256u, H);
+    const dim3 grid((row_u + 255u) / 256u, H < 65535u ? H : 65535u);  // grid.y limit: rows by grid stride
     if (wide)
         hipLaunchKernelGGL(place_tiles_kernel<uint4>, grid, dim3(256), 0, stream,
                            static_cast<const uint4*>(gathered), static_cast<uint4*>(frame), row_u,
@@ -916,14 +872,11 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     // unless another layout is forced
     if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) geo = kGeoTriBvh;
     size_t lds_total = lds_bytes;
-    // sphere BVH in LDS (1024-thread workgroups, two per CU) when it fits
-    if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto) {
-        const size_t b = sphere_lds_bytes(lds_bytes, P.nE, RT_SPH_BLOCK);
-        if (b <= kSphLdsMaxBytes) {
-            geo = kGeoSphLds;
-            lds_total = b;
-        }
-    }
+    // the sphere kernel (one-wave workgroups, compact BVH in L2) while its
+    // per-workgroup copy of the pair records is small (rt_kernel.hpp)
+    if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto &&
+        lds_bytes <= kSphPairLdsMaxBytes)
+        geo = kGeoSphLds;
     // box clusters whenever rt_create found some; not with
     // spheres, where the sphere walks dominate and the cluster code's register
     // pressure measured 4.6 % slower than the culled pair loop (config 4)

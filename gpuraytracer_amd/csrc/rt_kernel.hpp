@@ -15,77 +15,20 @@ constexpr size_t kMaxLdsBytes = 64 * 1024;
 constexpr uint32_t kOutFp16 = 0x2u;
 constexpr uint32_t kOutRgba8 = 0x10u;  // fused image.swift:35-65 epilogue, uchar4 store
 constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padded AABB
-// dynamic LDS of the sphere-BVH-in-LDS kernel: two 1024-thread workgroups per
-// CU share 160 KB with their static per-pixel sums (3 KB at 4 lanes per pixel)
-// and per-lane seeds (4 KB): 80 KB - 7 KB each
-constexpr size_t kSphLdsMaxBytes = 73 * 1024;
-// Per-lane sphere walks split across the lanes of a wave (rt_trace.hpp
-// sphere_walk_lds): each wave of the LDS-sphere kernel owns a 576-B LDS
-// scratch (64 B rank map + 64 u64 result slots), and the sphere ids of the
-// compact BVH entries are then read from global memory instead of LDS.
-#ifndef RT_SPH_SPLIT
-#define RT_SPH_SPLIT 0  // measured: wave steps -40 %, no faster; opt-in
-#endif
-constexpr uint32_t kWaveScratchBytes = 576;
-// Workgroup walk pool (rt_trace.hpp sphere_walk_pool): a
-// wave hands its last sphere walks of a query to an LDS pool that idle lanes
-// of every wave of the workgroup take from.  The pool holds every lane's
-// query slot, so the compact BVH moves to global memory (8 layouts, L2).
-#ifndef RT_SPH_POOL
-#define RT_SPH_POOL 0
-#endif
-#if RT_SPH_POOL && !defined(RT_SPH_LAYOUTS)
-#define RT_SPH_LAYOUTS 8
-#endif
-// pool bytes of one workgroup: per lane 16 B (o, best) + 16 B (d, entry) +
-// 4 B (id + 1, kind), per wave two 64-bit masks (handed over, finished), and
-// one 32-bit summary of the waves with handed-over walks (padded to 16 B)
-inline constexpr size_t sphere_pool_bytes(uint32_t block_threads) {
-    return (size_t)block_threads * 36u + (size_t)(block_threads / 64u) * 16u + 16u;
-}
-// Layouts of the compact sphere BVH (rt_scene.cpp build_sphere_lds): 8, one
-// per direction octant (256 KB at 1000 spheres), read from global memory
-// (L2-resident) with near/far boxes and 256-thread workgroups (round 3:
-// config 4 194 -> 161 ms) -- or 2, octants (+,+,+) and (-,-,-),
-// staged in LDS by 1024-thread workgroups (the round-2 kernel, opt-in).
-#ifndef RT_SPH_LAYOUTS
-#define RT_SPH_LAYOUTS 8
-#endif
-static_assert(!RT_SPH_POOL || RT_SPH_LAYOUTS == 8, "the walk pool takes the LDS of the 2-layout tree");
-// Near/far boxes (rt_scene.cpp build_sphere_lds): with one layout per direction
-// octant, each layout stores a box's entry planes in the lo slots, and the
-// per-lane walks (whose layout is their ray's octant) test the slab with
-// 4 min/max instead of 10 (rt_trace.hpp lds_node_hit_nf).
-#ifndef RT_SPH_NEARFAR
-#define RT_SPH_NEARFAR (RT_SPH_LAYOUTS == 8 ? 1 : 0)
-#endif
-static_assert(!RT_SPH_NEARFAR || RT_SPH_LAYOUTS == 8, "near/far boxes need one layout per octant");
-// dynamic LDS of the LDS-sphere kernel: pair records, both layouts of the
-// compact BVH, then the wave scratch (RT_SPH_SPLIT) or the entry ids
-inline size_t sphere_lds_bytes(size_t pair_bytes, uint32_t n_entries, uint32_t block_threads) {
-    if (RT_SPH_POOL) return pair_bytes + sphere_pool_bytes(block_threads);
-    if (RT_SPH_LAYOUTS == 8) return pair_bytes;  // entries and ids stay in global memory
-    const size_t ent = 2u * (size_t)n_entries * 16u;
-    return pair_bytes + ent +
-           (RT_SPH_SPLIT ? (size_t)(block_threads / 64u) * kWaveScratchBytes
-                         : ((2u * (size_t)n_entries * 2u + 3u) & ~(size_t)3u));
-}
-// threads per workgroup of the sphere kernel: 1024 (4x4 waves, two per CU)
-// when one LDS copy of the 2-layout tree serves 16 waves; ONE wave with the
-// tree in L2 -- a workgroup's wave slots and LDS stay taken until its slowest
-// wave ends, and the sphere walks make wave times differ a lot (config 4:
-// 1024 threads 186.1 ms, 512 177.9, 256 162.1, 128 160.5, 64 158.4)
-#ifndef RT_SPH_BLOCK
-#define RT_SPH_BLOCK (RT_SPH_LAYOUTS == 8 ? 64 : 1024)
-#endif
-constexpr uint32_t kSphBlockThreads = RT_SPH_BLOCK;
+// The sphere kernel (kGeoSphLds): one-wave workgroups that stage only the
+// pair records in LDS and walk the compact sphere BVH (8 octant layouts) from
+// global memory (L2-resident).  A workgroup keeps its wave slots until its
+// slowest wave ends and sphere walks make wave times differ a lot (config 4:
+// 1024 threads 186.1 ms, 512 177.9, 256 162.1, 128 160.5, 64 158.4).  Every
+// workgroup stages its own copy of the pair records, so the kernel is taken
+// only while they are small (kSphPairLdsMaxBytes; config 4: 672 B): above it
+// the pair kernel with the 32-B-node sphere walks serves the scene.
+constexpr uint32_t kSphBlockThreads = 64;
+constexpr size_t kSphPairLdsMaxBytes = 4 * 1024;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
-// Compact layouts of the triangle BVH (rt_lbvh.hip, rt_trace.hpp tri_cbvh_*): 2
-// (octants +++ and ---, rays take the majority of their signs) or 8 (one per
-// direction octant), 16 B per node, stored after the 8 full 32-B layouts.
-#ifndef RT_TRI_COMPACT_LAYOUTS
-#define RT_TRI_COMPACT_LAYOUTS 8
-#endif
+// Compact layouts of the triangle BVH (rt_lbvh.hip, rt_trace.hpp tri_cbvh_*):
+// one per direction octant, 16 B per node, stored after the 8 full 32-B layouts.
+constexpr uint32_t kTriCompactLayouts = 8;
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
 constexpr uint32_t kTriBvhMinTriangles = 384;
@@ -99,7 +42,7 @@ struct KParams {
     const float4* sph_nodes;  // 2 float4 per sphere-BVH node (BvhNode)
     const uint32_t* sph_perm; // BVH leaf order -> sphere id
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
-    const uint32_t* sph_lds;  // compact sphere BVH (2 layouts x nE x 16 B) for LDS, or null
+    const uint32_t* sph_lds;  // compact sphere BVH (8 layouts x nE x 16 B), or null
     const uint16_t* sph_lds_id;  // sphere id per compact entry
     const float4* tri_nodes;  // triangle BVH (rt_lbvh.hip): 8 layouts x nTN nodes, or null
     const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
@@ -108,7 +51,7 @@ struct KParams {
     float4* sum;              // running sums (tile layout) or null
     void* out;                // rgba32F / rgba16F tile or null
     uint32_t nT, nP, nS, nN;  // triangles, triangle pairs (0: no pair layout), spheres, BVH nodes
-    uint32_t nE;              // entries per layout of the compact LDS sphere BVH
+    uint32_t nE;              // entries per layout of the compact sphere BVH
     uint32_t nTN;             // triangle-BVH nodes per layout (0: no triangle BVH)
     float cam_pos[3], cam_u[3], cam_v[3], cam_w[3];
     float halfW, halfH;

@@ -157,13 +157,13 @@ __global__ void layout_kernel(uint32_t n, const uint32_t* __restrict__ child,
     float4* o = nodes + 2 * ((size_t)oct * total + idx);
     o[0] = make_float4(b0.x, b0.y, b0.z, __uint_as_float(escape));
     o[1] = make_float4(b1.x, b1.y, b1.z, __uint_as_float(leaf));
-    if (RT_TRI_COMPACT_LAYOUTS == 8 || oct == 0 || oct == 7) {
-        // compact 16-B entries (every octant's layout, or only those of (+,+,+)
-        // and (-,-,-)), after the 8 full layouts (rt_trace.hpp tri_cbvh_*): the box in fp16 rounded
-        // outward (a superset of the padded box), then escape | 2^31 for an
-        // inner node (an entry index over all compact layouts) or the leaf's triangle
-        // index in leaf order (a leaf's escape is the next entry)
-        const uint32_t lay = RT_TRI_COMPACT_LAYOUTS == 8 ? oct : (oct == 7 ? 1u : 0u);
+    {
+        // compact 16-B entries (every octant's layout), after the 8 full layouts
+        // (rt_trace.hpp tri_cbvh_*): the box in fp16 rounded outward (a
+        // superset of the padded box), then escape | 2^31 for an inner node (an
+        // entry index over all compact layouts) or the leaf's triangle index in
+        // leaf order (a leaf's escape is the next entry)
+        const uint32_t lay = oct;
         uint4* cn = reinterpret_cast<uint4*>(nodes + 2 * (size_t)8 * total) + (size_t)lay * total + idx;
         const uint32_t h0 = __half_as_ushort(__float2half_rd(b0.x)), h1 = __half_as_ushort(__float2half_rd(b0.y));
         const uint32_t h2 = __half_as_ushort(__float2half_rd(b0.z)), h3 = __half_as_ushort(__float2half_ru(b1.x));

@@ -22,10 +22,6 @@
 #include "rt_kernel.hpp"
 #include "rt_trace.hpp"
 
-#ifndef RT_MIS_SUM_LDS
-#define RT_MIS_SUM_LDS 1  // the cosine / VNDF strategy sums accumulate in the stash (slots 12-14)
-#endif
-
 namespace rt {
 
 namespace {
@@ -305,7 +301,7 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         st[10 * kBlockThreads + k] = dl.y;
         st[11 * kBlockThreads + k] = dl.z;
     }
-    if (RT_MIS_SUM_LDS) stash_set(sv, 12, f3{0.0f, 0.0f, 0.0f});
+    stash_set(sv, 12, f3{0.0f, 0.0f, 0.0f});  // the strategy sum accumulates in the stash
     for (uint32_t i = 0; i < S; ++i) {  // cosine-hemisphere sampling (:562-591)
         const float4 u = tab[3 * i + 1];
         const MisHit x = load_x(sv, xid);
@@ -319,13 +315,9 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float dl_pdf = light_pdf(P, x.p, dir);
         const float v_pdf = vndf_pdf(V, n, dir, hit_m(sv, x).roughness);
         const float w = power_h(cos_pdf, dl_pdf, v_pdf, nS);
-#if RT_MIS_SUM_LDS
         stash_add(sv, 12, continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w));
-#else
-        cs = cs + continue_sample<GEO>(P, sv, x, origin, dir, cos_pdf, w, u.z, u.w);
-#endif
     }
-    if (RT_MIS_SUM_LDS) cs = stash_get(sv, 12);
+    cs = stash_get(sv, 12);
     {  // (directLight + cosine) + vndf (:624), same order; dc waits in the stash
         const uint32_t k0 = opaque_lane_slot();
         const f3 dl2{sv.xstash[9 * kBlockThreads + k0], sv.xstash[10 * kBlockThreads + k0],
@@ -337,7 +329,7 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         st[10 * kBlockThreads + k] = dc.y;
         st[11 * kBlockThreads + k] = dc.z;
     }
-    if (RT_MIS_SUM_LDS) stash_set(sv, 12, f3{0.0f, 0.0f, 0.0f});
+    stash_set(sv, 12, f3{0.0f, 0.0f, 0.0f});  // the strategy sum accumulates in the stash
     for (uint32_t i = 0; i < S; ++i) {  // VNDF sampling (:593-623)
         const float4 u = tab[3 * i + 2];
         const MisHit x = load_x(sv, xid);
@@ -352,13 +344,9 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
         const float cos_pdf = cosine_pdf(n, dir);
         const float dl_pdf = light_pdf(P, x.p, dir);
         const float w = power_h(v_pdf, dl_pdf, cos_pdf, nS);
-#if RT_MIS_SUM_LDS
         stash_add(sv, 12, continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w));
-#else
-        vn = vn + continue_sample<GEO>(P, sv, x, origin, dir, v_pdf, w, u.z, u.w);
-#endif
     }
-    if (RT_MIS_SUM_LDS) vn = stash_get(sv, 12);
+    vn = stash_get(sv, 12);
     const uint32_t k = opaque_lane_slot();
     const f3 dc{sv.xstash[9 * kBlockThreads + k], sv.xstash[10 * kBlockThreads + k],
                 sv.xstash[11 * kBlockThreads + k]};
@@ -368,17 +356,14 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
 
 }  // namespace
 
-#ifndef RT_MIS_LANES
-#define RT_MIS_LANES 2  // lanes per pixel (1, 2, 4 or 8)
-#endif
-#ifndef RT_MIS_WAVES_PER_EU
+// lanes per pixel: 2 (20.3 ms per reference frame; 1 lane 26.1, 4 lanes 25.7)
+constexpr uint32_t kMisLanes = 2;
 // 7 waves/SIMD: 72 VGPRs without scratch since the primary hit, the pixel sum,
 // dl/dc and the running strategy sum wait in the per-lane LDS stash (round 2:
 // 120 VGPRs at 4 waves; 6 waves then spilled 54 VGPRs).  DESIGN.md §5
-#define RT_MIS_WAVES_PER_EU 7
-#endif
+constexpr int kMisWavesPerEu = 7;
 template <int GEO>
-__global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel(MisParams P) {
+__global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
     sv.nT = P.nT;
@@ -432,7 +417,7 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     // Pixel of a lane; recomputed from an opaque threadIdx where it is used
     // (as in rt_kernel.hip), not held across the camera-ray loop.  A wave is
     // 8 x (8 / ML) pixels, a workgroup 2 x 2 waves.
-    constexpr uint32_t ML = RT_MIS_LANES;
+    constexpr uint32_t ML = kMisLanes;
     constexpr uint32_t kWY = 8u / ML;
     auto pixel_of = [&](uint32_t tid, uint32_t& x, uint32_t& j) {
         const uint32_t lane = tid & 63u, wave = tid >> 6, pix = lane / ML;
@@ -544,33 +529,41 @@ __global__ __launch_bounds__(kBlockThreads, RT_MIS_WAVES_PER_EU) void mis_kernel
     }
 }
 
-constexpr size_t kMisStashBytes = (RT_MIS_SUM_LDS ? 15u : 12u) * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc (+ strategy sum)
+constexpr size_t kMisStashBytes = 15u * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc, strategy sum
 
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + shading records
     return (size_t)((n_pairs ? kPairF4 * n_pairs : 3u * n_tri) + 3u * n_tri) * sizeof(float4);
 }
 
-hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
-    constexpr uint32_t TY = 2u * (8u / RT_MIS_LANES);  // workgroup: 16 x TY pixels
+// Dynamic LDS above 64 KB must be allowed per kernel: a scene whose records
+// fit the 64 KB of the LDS layouts keeps them with the 15 KB stash on top
+// (up to 79 KB per workgroup, fewer workgroups per CU) instead of dropping to
+// the global-memory kernel.
+template <int GEO>
+hipError_t launch_mis_g(const MisParams& P, size_t lds, hipStream_t stream) {
+    constexpr uint32_t TY = 2u * (8u / kMisLanes);  // workgroup: 16 x TY pixels
     const dim3 grid((P.W + 15u) / 16u, (P.row_count + TY - 1) / TY);
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute((const void*)mis_kernel<GEO>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(mis_kernel<GEO>, grid, dim3(kBlockThreads), lds, stream, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
     const bool pairs = mem != SceneMem::kLdsSingle && P.nP > 0;
     const size_t lds = mis_lds_bytes(P.nT, pairs ? P.nP : 0u);
     const bool lds_ok = mem != SceneMem::kSmem && lds <= kMaxLdsBytes;
     const size_t X = kMisStashBytes;
-    if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) {
-        hipLaunchKernelGGL(mis_kernel<kGeoTriBvh>, grid, dim3(kBlockThreads), X, stream, P);
-    } else if (lds_ok && lds + X <= kMaxLdsBytes) {
-        const size_t lds_clu = lds + kCluF4 * P.nC * sizeof(float4);
-        if (pairs && P.nC > 0 && mem == SceneMem::kAuto && lds_clu + X <= kMaxLdsBytes)
-            hipLaunchKernelGGL(mis_kernel<kGeoPairClu>, grid, dim3(kBlockThreads), lds_clu + X, stream, P);
-        else if (pairs)
-            hipLaunchKernelGGL(mis_kernel<kGeoPairLds>, grid, dim3(kBlockThreads), lds + X, stream, P);
-        else
-            hipLaunchKernelGGL(mis_kernel<kGeoTriLds>, grid, dim3(kBlockThreads), lds + X, stream, P);
-    } else {
-        hipLaunchKernelGGL(mis_kernel<kGeoTriGlobal>, grid, dim3(kBlockThreads), X, stream, P);
-    }
-    return hipGetLastError();
+    if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) return launch_mis_g<kGeoTriBvh>(P, X, stream);
+    if (!lds_ok) return launch_mis_g<kGeoTriGlobal>(P, X, stream);
+    const size_t lds_clu = lds + kCluF4 * P.nC * sizeof(float4);
+    if (pairs && P.nC > 0 && mem == SceneMem::kAuto && lds_clu <= kMaxLdsBytes)
+        return launch_mis_g<kGeoPairClu>(P, lds_clu + X, stream);
+    if (pairs) return launch_mis_g<kGeoPairLds>(P, lds + X, stream);
+    return launch_mis_g<kGeoTriLds>(P, lds + X, stream);
 }
 
 }  // namespace rt

@@ -435,10 +435,8 @@ static void build_sphere_lds(CompiledScene* out) {
     if (ne > 0x7FFFu) return;
     std::vector<uint32_t> ent;
     std::vector<uint16_t> ids;
-    const int octs2[2] = {0, 7}, octs8[8] = {0, 1, 2, 3, 4, 5, 6, 7};
-    const int nlay = RT_SPH_LAYOUTS == 8 ? 8 : 2;
-    for (int li = 0; li < nlay; ++li) {
-        const int oct = nlay == 8 ? octs8[li] : octs2[li];
+    for (int li = 0; li < 8; ++li) {  // one layout per direction octant
+        const int oct = li;
         // escapes are entry indices of the concatenated layouts (layout li
         // starts at li * ne), so a walk's position alone names its layout
         const uint32_t lay_base = (uint32_t)li * ne;
@@ -458,10 +456,10 @@ static void build_sphere_lds(CompiledScene* out) {
                     if (!isfinite(n.lo[a]) || !isfinite(n.hi[a])) return;
                     h[a] = half_dir(n.lo[a], -1);
                     h[3 + a] = half_dir(n.hi[a], +1);
-                    // RT_SPH_NEARFAR: in the layout of octant `oct` the box plane a ray
+                    // near/far boxes: in the layout of octant `oct` the box plane a ray
                     // of that octant enters through (hi when component a is negative)
                     // takes the lo slot, so the walk's slab test needs no min/max pairs
-                    if (RT_SPH_NEARFAR && ((oct >> a) & 1)) std::swap(h[a], h[3 + a]);
+                    if ((oct >> a) & 1) std::swap(h[a], h[3 + a]);
                 }
                 if (n.escape > nn) return;
                 const uint32_t w[4] = {h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,

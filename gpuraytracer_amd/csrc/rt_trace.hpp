@@ -85,11 +85,7 @@ __device__ __forceinline__ bool bary_ok(float den, uint32_t t1, uint32_t t2) {
 __device__ __forceinline__ float pair_t(f3 n, f3 tv, float den) {
     const uint32_t nsgn = (__float_as_uint(den) & 0x80000000u) ^ 0x80000000u;
     const float tn = __uint_as_float(__float_as_uint(dot(n, tv)) ^ nsgn);
-#ifdef RT_TIMING_APPROX_DIV  // timing-only experiment, NOT bit-exact
-    return tn * __builtin_amdgcn_rcpf(fabsf(den));
-#else
     return tn / fabsf(den);
-#endif
 }
 
 // intersectSphere (shaders_old.metal:108-136) with the DESIGN.md §3.6 root rule.
@@ -112,16 +108,17 @@ __device__ __forceinline__ bool sph_test(const float4& S, f3 o, f3 d, float a, f
     return false;
 }
 
-// Diagnostic counters (only in an -DRT_STATS build; read with rt_debug_stats).
+// Diagnostic counters (only in an -DRT_STATS instrumentation build, read with
+// rt_debug_stats by tools/kernel_stats.py and tools/sphere_stats.py).
 // Slot groups of 4 per query kind q (0: camera closest hit, 1: bounce closest
 // hit, 2: shadow any-hit): [4q] pair records visited per wave, [4q+1] records
 // tested, [4q+2] active lanes summed over tested records, [4q+3] division blocks.
 // Box-cluster queries: [12] queries per wave, [13] candidate rounds per wave,
 // [14] lanes summed over rounds, [15] lanes summed over queries.
-// Sphere walks (sphere_walk_lds), base 16 closest / 24 any-hit: [+0] walks per
-// wave, [+1] lanes summed over walks, [+2] cheap-step iterations, [+3] lanes
+// Sphere walks (sphere_walk), base 16 closest / 24 any-hit: [+0] walks per
+// wave, [+1] lanes summed over walks, [+2] walk-loop iterations, [+3] lanes
 // summed over them, [+4] unused, [+5] root rounds, [+6] parked lanes summed
-// over them.  [23] packet walks, [31] packet walk iterations.
+// over them.
 #ifdef RT_STATS
 __device__ unsigned long long g_rt_stats[32];
 __device__ __forceinline__ void stat_wave(int slot, unsigned long long v) {
@@ -141,7 +138,7 @@ enum Geo : int {
     kGeoTriBvh = 5,     // GPU-built triangle BVH (rt_lbvh.hip), records from global
     kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
     kGeoPairClu = 6,    // pair records in LDS + box clusters
-    kGeoSphLds = 7,     // pair records + the compact sphere BVH in LDS (1024-thread workgroups)
+    kGeoSphLds = 7,     // pair records in LDS + the compact sphere BVH in L2 (one-wave workgroups)
 };
 
 constexpr bool geo_pairs(int g) { return g == kGeoPairLds || g == kGeoPairSmem || g == kGeoSphLds; }
@@ -161,10 +158,8 @@ struct SceneView {
     uint32_t nC;
     uint32_t pair_free;       // pairs in no cluster: tested by every lane
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
-    const uint4* sent;        // compact sphere BVH entries in LDS (kGeoSphLds), 2 layouts
-    const uint16_t* sid;      // sphere id of each entry (leaves): LDS, or global with RT_SPH_SPLIT
-    uint8_t* wscr;            // this wave's LDS scratch for split walks (kWaveScratchBytes)
-    uint8_t* pool;            // the workgroup's walk pool in LDS (RT_SPH_POOL, sphere_pool_bytes)
+    const uint4* sent;        // compact sphere BVH entries (kGeoSphLds): 8 octant layouts, global
+    const uint16_t* sid;      // sphere id of each compact entry (leaves), global
     const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
     float* xstash;            // MIS: per-lane primary hit (p, din), SoA in LDS (rt_mis.hip)
 };
@@ -177,44 +172,25 @@ struct SceneView {
 // finite scene data (no signalling NaNs), for which v_min/v_max_f32 return
 // exactly fminf/fmaxf; and these values only decide what is culled, never a
 // result.
-#ifndef RT_ASM_MINMAX
-#define RT_ASM_MINMAX 1
-#endif
 __device__ __forceinline__ float vmin(float a, float b) {
-#if RT_ASM_MINMAX
     float r;
     asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
-#else
-    return fminf(a, b);
-#endif
 }
 __device__ __forceinline__ float vmax(float a, float b) {
-#if RT_ASM_MINMAX
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
-#else
-    return fmaxf(a, b);
-#endif
 }
 __device__ __forceinline__ float vmin3(float a, float b, float c) {
-#if RT_ASM_MINMAX
     float r;
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-#else
-    return fminf(fminf(a, b), c);
-#endif
 }
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
-#if RT_ASM_MINMAX
     float r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-#else
-    return fmaxf(fmaxf(a, b), c);
-#endif
 }
 
 // Per-ray data of the slab test.  1/d uses the 1-ulp hardware reciprocal: the
@@ -246,14 +222,6 @@ __device__ __forceinline__ bool node_hit(const float4& n0, const float4& n1, con
     return tnear <= tfar;
 }
 
-#ifndef RT_SPH_PACKET
-// sphere scenes: 1: wave-packet walks for camera and bounce-0 shadow rays;
-// 2: + all shadow rays; 3: all; 0 (round 3): per-lane walks for every ray --
-// with the near/far L2 tree and one-wave workgroups 155.8 vs 158.4 ms on
-// config 4.  (Triangle-BVH scenes keep packets for bounce-0 shadow rays.)
-#define RT_SPH_PACKET 0
-#endif
-
 // BVH layout of a ray direction: bit a set when component a is negative.
 __device__ __forceinline__ uint32_t octant(f3 d) {
     return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
@@ -264,31 +232,27 @@ __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
-// Sphere-BVH walks.  The wave walks ONE stackless
-// depth-first path through the escape-index tree: a node is entered when any
-// active lane's ray may hit its padded box.  The node index is therefore wave
-// uniform, node and sphere records are fetched with scalar loads from global
-// memory (no LDS footprint, no bank conflicts) and every lane stays busy; a
-// lane whose own box test failed still tests the leaf's spheres, which cannot
-// change its result because the boxes are conservative.
-template <bool PACKET>
+// Sphere-BVH walks over the 32-B nodes (the sphere scenes of the pair, single
+// and global layouts; the default sphere kernel walks the compact BVH below).
+// One stackless depth-first walk per lane through the escape-index tree of
+// the ray's direction octant (near child first); a node is entered when the
+// ray may hit its padded box.  Candidates are ranked by (t, sphere id) exactly
+// like the oracle's id-ordered scan with strict '<', so the visiting order is
+// free.
 __device__ __forceinline__ void sphere_closest(const float4* __restrict__ node,
                                                const float4* __restrict__ sph,
                                                const uint32_t* __restrict__ perm, uint32_t nN,
                                                uint32_t nT, f3 o, f3 d, float tmin, float& best,
                                                int& id) {
-    // Candidates are ranked by (t, sphere id) exactly like the oracle's
-    // id-ordered scan with strict '<', so the visiting order is free.
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
-    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
+    node += 2u * nN * octant(d);
     uint32_t idx = 0;
     while (idx < nN) {
         const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
-        uint32_t next = PACKET ? wave_uniform(__float_as_uint(n0.w)) : __float_as_uint(n0.w);
-        const bool h = node_hit(n0, n1, rb, tmin, best);
-        if (PACKET ? __builtin_amdgcn_ballot_w64(h) != 0 : h) {
-            const uint32_t leaf = PACKET ? wave_uniform(__float_as_uint(n1.w)) : __float_as_uint(n1.w);
+        uint32_t next = __float_as_uint(n0.w);
+        if (node_hit(n0, n1, rb, tmin, best)) {
+            const uint32_t leaf = __float_as_uint(n1.w);
             if (leaf == 0u) {
                 next = idx + 1;
             } else {
@@ -309,71 +273,41 @@ __device__ __forceinline__ void sphere_closest(const float4* __restrict__ node,
     }
 }
 
-template <bool PACKET>
 __device__ __forceinline__ bool sphere_any(const float4* __restrict__ node,
                                            const float4* __restrict__ sph, uint32_t nN, f3 o,
                                            f3 d, float tmin, float tmax) {
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
-    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
-    bool found = false;
+    node += 2u * nN * octant(d);
     uint32_t idx = 0;
     while (idx < nN) {
         const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
-        if (PACKET) {
-            uint32_t next = wave_uniform(__float_as_uint(n0.w));
-            if (__builtin_amdgcn_ballot_w64(!found && node_hit(n0, n1, rb, tmin, tmax)) != 0) {
-                const uint32_t leaf = wave_uniform(__float_as_uint(n1.w));
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        found = found || sph_test(sph[k], o, d, a, tmin, tmax, &t);
-                    }
-                    if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
+        uint32_t next = __float_as_uint(n0.w);
+        if (node_hit(n0, n1, rb, tmin, tmax)) {
+            const uint32_t leaf = __float_as_uint(n1.w);
+            if (leaf == 0u) {
+                next = idx + 1;
+            } else {
+                const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
+                for (uint32_t k = first; k < end; ++k) {
+                    float t;
+                    if (sph_test(sph[k], o, d, a, tmin, tmax, &t)) return true;
                 }
             }
-            idx = next;
-        } else {
-            uint32_t next = __float_as_uint(n0.w);
-            if (node_hit(n0, n1, rb, tmin, tmax)) {
-                const uint32_t leaf = __float_as_uint(n1.w);
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        if (sph_test(sph[k], o, d, a, tmin, tmax, &t)) return true;
-                    }
-                }
-            }
-            idx = next;
         }
+        idx = next;
     }
-    return found;
+    return false;
 }
 
-// Sphere-BVH walks over the compact LDS entries (rt_scene.cpp build_sphere_lds):
-// the same stackless depth-first walk and (t, id) ranking as sphere_closest /
-// sphere_any, with fp16 boxes rounded outward (still conservative) and the
-// sphere of a leaf stored in the entry itself (a leaf's escape is the next
-// entry).  Two layouts: near child first for (+,+,+) and for (-,-,-); a ray
-// takes the one matching most of its direction signs.
+// Compact BVH entries (rt_scene.cpp build_sphere_lds, rt_lbvh.hip): 16 B per
+// node, an fp16 box rounded outward (still conservative) and one word --
+// escape | 2^31 for an inner node (the escape is an entry index over all
+// layouts, so a walk's position names its layout); a sphere leaf stores the
+// sphere (c, r*r) itself (a leaf's escape is the next entry).
 __device__ __forceinline__ float h2f(uint32_t b16) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)b16);
 }
-
-__device__ __forceinline__ uint32_t lds_layout(f3 d) {
-#ifdef RT_SPH_ONE_LAYOUT  // experiment: every ray walks layout (+,+,+) (speed only)
-    return 0u;
-#endif
-    return __builtin_popcount(octant(d)) >= 2 ? 1u : 0u;
-}
-// layout of the compact sphere BVH a ray walks (RT_SPH_LAYOUTS)
-__device__ __forceinline__ uint32_t sph_layout(f3 d) { return RT_SPH_LAYOUTS == 8 ? octant(d) : lds_layout(d); }
 
 __device__ __forceinline__ bool lds_node_hit(const uint4& e, const RayBox& rb, float tmin,
                                              float tmax) {
@@ -382,11 +316,11 @@ __device__ __forceinline__ bool lds_node_hit(const uint4& e, const RayBox& rb, f
     return node_hit(n0, n1, rb, tmin, tmax);
 }
 
-// Slab test of a near/far entry (RT_SPH_NEARFAR): the lo slots hold the planes
-// the ray enters through, which holds for every ray whose direction octant is
-// the layout's.  Equal to lds_node_hit for such rays: fma(p, invd, -oinv) is
-// monotone in p and sign(invd) orders the two planes of each axis, so the
-// min/max pairs of node_hit select exactly these values.
+// Slab test of a near/far entry: in the layout of direction octant k the lo
+// slots hold the planes a ray of that octant enters through.  Equal to
+// lds_node_hit for such rays: fma(p, invd, -oinv) is monotone in p and
+// sign(invd) orders the two planes of each axis, so the min/max pairs of
+// node_hit select exactly these values.
 __device__ __forceinline__ bool lds_node_hit_nf(const uint4& e, const RayBox& rb, float tmin,
                                                 float tmax) {
     const float nx = fmaf(h2f(e.x & 0xFFFFu), rb.invd.x, -rb.oinv.x);
@@ -398,119 +332,34 @@ __device__ __forceinline__ bool lds_node_hit_nf(const uint4& e, const RayBox& rb
     return vmax3(nx, ny, vmax(nz, tmin)) <= vmin3(fx, fy, vmin(fz, tmax));
 }
 
-template <bool PACKET>
-__device__ __forceinline__ void sphere_closest_lds(const uint4* ent, const uint16_t* ids,
-                                                   uint32_t nN, uint32_t nT, f3 o, f3 d,
-                                                   float tmin, float& best, int& id) {
+// Per-lane walk of the compact sphere BVH with POSTPONED ROOTS (DESIGN.md
+// §3.10; after Aila & Laine's postponed leaf processing, stackless form).
+// Each lane walks the layout of its ray's direction octant.  Each step of a
+// lane is cheap and of similar cost whatever the entry: a near/far box test
+// for an inner node, the discriminant of sph_test for a leaf.  A leaf whose
+// discriminant is positive (a real hit candidate) parks the lane with (b, disc);
+// the others walk on until at least 1/kSphParkDen of the lanes still
+// walking are parked (or none can move), then the wave runs the expensive part
+// of the sphere test -- the IEEE sqrt and divisions -- for all parked lanes
+// together.  Per lane the entries are visited in the same order and every
+// value is sph_test's, ranked by (t, id): the same result.  ANY: *id becomes
+// >= 0 on the first accepted hit (and that lane stops).
+// the parked roots run once they are >= 1/kSphParkDen of the live lanes
+// (config 4: 2 157.3 ms, 4 158.4, 6 161.1)
+constexpr int kSphParkDen = 2;
+template <bool ANY>
+__device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const uint16_t* __restrict__ ids,
+                                            uint32_t nN, uint32_t nT, f3 o, f3 d, float tmin, float& best,
+                                            int& id) {
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
     const float a = dot(d, d);
     const RayBox rb = ray_box(o, d);
-    const uint32_t lay = PACKET ? wave_uniform(sph_layout(d)) : sph_layout(d);
-    // entry indices (and escapes) run over both layouts: layout `lay` is
-    // [lay * nN, (lay + 1) * nN)
-    uint32_t idx = lay * nN;
-    const uint32_t end = idx + nN;
-    if (PACKET) RT_STAT(23, 1);
-    while (idx < end) {
-        if (PACKET) RT_STAT(31, 1);
-        const uint4 e = ent[idx];
-        uint32_t next = idx + 1;
-        if (e.w & 0x80000000u) {  // inner node (wave-uniform for PACKET)
-            const bool h = lds_node_hit(e, rb, tmin, best);
-            if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) next = e.w & 0x7FFFFFFFu;
-        } else {  // leaf: the sphere (c, r*r)
-            float t;
-            if (sph_test(make_float4(__uint_as_float(e.x), __uint_as_float(e.y),
-                                     __uint_as_float(e.z), __uint_as_float(e.w)),
-                         o, d, a, tmin, 3.0e38f, &t) && t <= best) {
-                const int s = (int)(nT + ids[idx]);
-                if (t < best || s < id) {
-                    best = t;
-                    id = s;
-                }
-            }
-        }
-        idx = PACKET ? wave_uniform(next) : next;
-    }
-}
-
-// Per-lane walk of the compact LDS BVH with POSTPONED ROOTS (DESIGN.md §3.10;
-// after Aila & Laine's postponed leaf processing, stackless form).  Each step
-// of a lane is cheap and of similar cost whatever the entry: a box test for an
-// inner node, the discriminant of sph_test for a leaf.  A leaf whose
-// discriminant is positive (a real hit candidate) parks the lane with (b, disc);
-// the others walk on until at least half of the lanes still walking are
-// parked (or none can move), then the wave runs the expensive part of the
-// sphere test -- the IEEE sqrt and divisions -- for all parked lanes together.
-// In the plain walk (sphere_closest_lds) a mixed wave pays for the box test,
-// the discriminant AND the roots in most steps.  Per lane the entries are
-// visited in the same order and every value is sph_test's, ranked by (t, id):
-// the same result.  ANY: *id becomes >= 0 on the first accepted hit (and that
-// lane stops).
-//
-// SPLIT: a wave no longer waits with idle lanes for its
-// longest walk.  A walk is a range [idx, end) of the depth-first entry order
-// (stackless: walking from any entry m to end visits everything of the
-// subtrees from m on that the full walk would, plus possibly more).  When at
-// least RT_SPH_SPLIT_MIN lanes of the wave have finished, every walking lane
-// offers the rest of its range after the current subtree ([escape, end); or
-// after the first child when the subtree is all that is left), and the k-th
-// idle lane takes the k-th offer: it pulls the ray, the running (best, id) and
-// the range through cross-lane reads (ds_bpermute), the giver keeps
-// [idx, split).  Takers may be split again.  At the end every lane delivers
-// its (t, id) to the walk's original lane with an LDS atomic min of the key
-// (t bits << 32 | id + 1) -- exactly the (t, id) ranking, since every t here
-// is positive -- and every lane reads back its own query's result.  Extra
-// entries visited by a split walk can only add candidates that are real hits
-// in (tmin, tmax), so the minimum is the brute-force one.
-#ifndef RT_SPH_PARK_DEN
-#define RT_SPH_PARK_DEN 2  // the parked roots run once they are >= 1/DEN of the live lanes (L2 tree: 2 157.3 ms, 4 158.4, 6 161.1)
-#endif
-#ifndef RT_SPH_SPLIT_CLOSEST_ONLY
-#define RT_SPH_SPLIT_CLOSEST_ONLY 0  // 1: shadow (any-hit) walks are not split
-#endif
-#ifndef RT_SPH_SPLIT_MIN
-#define RT_SPH_SPLIT_MIN 16  // idle lanes of a wave that trigger a split round
-#endif
-__device__ __forceinline__ unsigned long long walk_key(float best, int id) {
-    return ((unsigned long long)__float_as_uint(best) << 32) | (uint32_t)(id + 1);
-}
-
-template <bool ANY, bool SPLIT>
-__device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t* ids, uint32_t nN,
-                                                uint32_t nT, f3 o, f3 d, float tmin, float& best,
-                                                int& id, uint8_t* wscr) {
-    constexpr uint32_t kNone = 0xFFFFFFFFu;
-#ifdef RT_TIMING_NO_SPH_WALK  // timing-only experiment (share of the walks), NOT exact
-    return;
-#endif
-#ifdef RT_TIMING_NO_SPH_ANY  // timing-only: share of the per-lane shadow walks, NOT exact
-    if (ANY) return;
-#endif
-#ifdef RT_TIMING_NO_SPH_CLOSEST  // timing-only: share of the per-lane closest walks, NOT exact
-    if (!ANY) return;
-#endif
-    float a = dot(d, d);
-    RayBox rb = ray_box(o, d);
     // entry range of this lane's walk over the concatenated layouts
-    uint32_t idx = sph_layout(d) * nN;
-    uint32_t end = idx + nN;
+    uint32_t idx = octant(d) * nN;
+    const uint32_t end = idx + nN;
     if (ANY && id >= 0) idx = end;
     uint32_t leaf = kNone;                      // the parked leaf
     float pb = 0.0f, pdisc = 0.0f;              // its b and discriminant
-    [[maybe_unused]] const uint32_t lane = __lane_id();
-    [[maybe_unused]] uint32_t owner = lane;     // lane whose query this walk serves
-    [[maybe_unused]] bool split_any = false;    // wave-uniform
-    // the wave scratch as LDS pointers (a generic pointer would become flat
-    // accesses): rank map [64] bytes, then 64 result keys
-    typedef __attribute__((address_space(3))) uint8_t lds_u8;
-    typedef __attribute__((address_space(3))) unsigned long long lds_u64;
-    lds_u8* rank_map = (lds_u8*)wscr;
-    lds_u64* res = (lds_u64*)(wscr + 64);
-    [[maybe_unused]] const int n_exec = __popcll(__builtin_amdgcn_ballot_w64(true));
-    // split when RT_SPH_SPLIT_MIN more lanes are idle than the last round
-    // left without work (no offer for them): a wave whose remaining walks
-    // cannot be split any more does not retry every step
-    [[maybe_unused]] int split_at = RT_SPH_SPLIT_MIN;  // wave-uniform
     [[maybe_unused]] constexpr int ST = ANY ? 24 : 16;
     RT_STAT(ST, 1);
     RT_STAT(ST + 1, __popcll(__ballot(1)));
@@ -523,9 +372,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             if (adv) {
                 const uint4 e = ent[idx];
                 if (e.w & 0x80000000u) {
-                    const bool h = RT_SPH_NEARFAR && !SPLIT ? lds_node_hit_nf(e, rb, tmin, best)
-                                                            : lds_node_hit(e, rb, tmin, best);
-                    idx = h ? idx + 1 : (e.w & 0x7FFFFFFFu);
+                    idx = lds_node_hit_nf(e, rb, tmin, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
                 } else {  // sph_test up to the discriminant (shaders_old.metal:108-136)
                     const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y),
                                          __uint_as_float(e.z)};
@@ -542,77 +389,7 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             }
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
-            if (RT_SPH_PARK_DEN * parked >= live) break;
-            if constexpr (SPLIT) {
-                if (n_exec - live >= split_at) {  // lanes with nothing to walk
-                    RT_STAT(ST + 4, 1);
-                    const bool idle = idx >= end && leaf == kNone;
-                    const unsigned long long idle_m = __builtin_amdgcn_ballot_w64(idle);
-                    if (!split_any) {  // first split of this walk: empty result slots
-                        res[lane] = ANY ? 0ull : ~0ull;
-                        split_any = true;
-                    }
-                    // offer: the part of the range after the current subtree
-                    uint32_t m = end;
-                    if (idx < end && leaf == kNone) {
-                        const uint4 e = ent[idx];
-                        if (e.w & 0x80000000u) {
-                            const uint32_t esc = e.w & 0x7FFFFFFFu;
-                            if (esc < end) {
-                                m = esc;
-                            } else {  // the subtree is all that is left: offer its 2nd child on
-                                const uint32_t w1 = ent[idx + 1].w;
-                                m = (w1 & 0x80000000u) ? (w1 & 0x7FFFFFFFu) : idx + 2;
-                            }
-                        } else {
-                            m = idx + 1;
-                        }
-                    }
-                    const bool can = m < end;
-                    const unsigned long long can_m = __builtin_amdgcn_ballot_w64(can);
-                    const uint32_t n = (uint32_t)min(__popcll(can_m), __popcll(idle_m));
-                    const uint32_t rc = __builtin_amdgcn_mbcnt_hi((uint32_t)(can_m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)can_m, 0u));
-                    const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle_m >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle_m, 0u));
-                    const bool giver = can && rc < n;
-                    const bool taker = idle && ri < n;
-                    split_at = (__popcll(idle_m) - (int)n) + RT_SPH_SPLIT_MIN;
-                    if (giver) rank_map[rc] = (uint8_t)lane;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    const int src = taker ? (int)rank_map[ri] : (int)lane;
-                    // the taker's finished query result goes to its query's lane
-                    if (taker) {
-                        if (ANY)
-                            __hip_atomic_fetch_max(&res[owner], id >= 0 ? 1ull : 0ull, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
-                        else
-                            __hip_atomic_fetch_min(&res[owner], walk_key(best, id), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    }
-                    // the giver's ray, running (best, id), split point, range end
-                    // and query lane (two 16-bit fields per word where they fit)
-                    const f3 o2{__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src)};
-                    const f3 d2{__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src)};
-                    const float best2 = __shfl(best, src);
-                    const uint32_t range2 = (uint32_t)__shfl((int)(m | (end << 16)), src);
-                    const uint32_t who2 = (uint32_t)__shfl((int)(owner | ((uint32_t)(id + 1) << 8)), src);
-                    if (taker) {
-                        o = o2;
-                        d = d2;
-                        a = dot(d, d);
-                        rb = ray_box(o, d);
-                        best = best2;
-                        id = (int)(who2 >> 8) - 1;
-                        idx = range2 & 0xFFFFu;
-                        end = range2 >> 16;
-                        owner = who2 & 0xFFu;
-                    }
-                    if (giver) end = m;
-                }
-            }
+            if (kSphParkDen * parked >= live) break;
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
         RT_STAT(ST + 5, 1);
@@ -637,472 +414,33 @@ __device__ __forceinline__ void sphere_walk_lds(const uint4* ent, const uint16_t
             leaf = kNone;
         }
     }
-    if constexpr (SPLIT) {
-        if (split_any) {  // every walk's (t, id) to its query's lane; read back this lane's own
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (ANY)
-                __hip_atomic_fetch_max(&res[owner], id >= 0 ? 1ull : 0ull, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
-            else
-                __hip_atomic_fetch_min(&res[owner], walk_key(best, id), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const unsigned long long k = res[lane];
-            if (ANY) {
-                id = k ? 0 : -1;
-            } else {
-                best = __uint_as_float((uint32_t)(k >> 32));
-                id = (int)(uint32_t)k - 1;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Workgroup walk pool (RT_SPH_POOL).  A wave's per-lane walks
-// take as long as its longest one (a lane walks ~38 entries, its wave ~103):
-// the lanes that finish early idle.  Here every lane's query sits in its own
-// LDS slot; once at most RT_SPH_POOL_T walks of a wave are left, the wave hands
-// them to the workgroup's pool (slot state + a bit in its `ready` mask) and
-// its idle lanes -- like those of every wave of the workgroup that has handed
-// over -- claim handed-over walks, of any wave and of either kind, and walk
-// them to the end.  The result goes back to the query's slot (and a bit in
-// the owner's `done` mask); every lane finally reads its own query back.
-// Packing the tails of 16 waves into few dense waves is the point: the
-// waiting waves issue nothing (s_sleep) and leave their SIMD to others.
-//
-// Exactness: a walk is the same sequence of entries and the same arithmetic
-// whichever lane runs it (the ray, running best and entry index travel
-// bit-exactly through LDS; a and the slab constants are recomputed from d
-// by the same code), so results are those of sphere_walk_lds.  tmin of a
-// pooled walk is implied by its kind: 0 for shadow (any-hit) walks
-// (raytrace.metal:79-85 leaves min_distance at 0) and 1e-3 for closest walks
-// (sampling.metal:154) -- the only two queries of the path.  The box tests
-// use tmin 0 for both (a superset of the entries: conservative).
-//
-// Liveness: a claimed walk always ends (entry indices only grow), a wave
-// never leaves the walk while it holds claimed walks, and a wave waiting for
-// its own handed-over walks claims them itself when nobody else has.
-#ifndef RT_SPH_POOL_T
-#define RT_SPH_POOL_T 16      // hand over once <= T walks of the wave are left
-#endif
-#ifndef RT_SPH_POOL_REFILL
-#define RT_SPH_POOL_REFILL 8  // idle lanes (beyond the last claim) that trigger another claim
-#endif
-
-typedef __attribute__((address_space(3))) float4 lds_f4_t;
-typedef __attribute__((address_space(3))) float lds_f32_t;
-typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
-typedef __attribute__((address_space(3))) unsigned long long lds_u64_t;
-
-struct PoolView {
-    lds_f4_t* a;      // [NT] o, best
-    lds_f4_t* b;      // [NT] d, entry index (bits)
-    lds_u32_t* c;     // [NT] id + 1 | any-hit << 31
-    lds_u64_t* ready; // [NW] handed-over walks not claimed yet (bit = lane)
-    lds_u64_t* done;  // [NW] handed-over walks finished
-    lds_u32_t* sum;   // waves with ready walks (bit = wave)
-};
-
-template <uint32_t NT>
-__device__ __forceinline__ PoolView pool_view(uint8_t* base) {
-    typedef __attribute__((address_space(3))) uint8_t lds_u8_t;
-    lds_u8_t* p = (lds_u8_t*)base;
-    PoolView v;
-    v.a = (lds_f4_t*)p;
-    v.b = (lds_f4_t*)(p + 16u * NT);
-    v.c = (lds_u32_t*)(p + 32u * NT);
-    v.ready = (lds_u64_t*)(p + 36u * NT);
-    v.done = (lds_u64_t*)(p + 36u * NT + 8u * (NT / 64u));
-    v.sum = (lds_u32_t*)(p + 36u * NT + 16u * (NT / 64u));
-    return v;
-}
-
-// Zero the masks (every thread of the workgroup calls it before the first
-// __syncthreads of the kernel).
-template <uint32_t NT>
-__device__ __forceinline__ void pool_init(uint8_t* base, uint32_t tid) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const PoolView v = pool_view<NT>(base);
-    if (tid < NT / 64u) {
-        v.ready[tid] = 0ull;
-        v.done[tid] = 0ull;
-    }
-    if (tid == 0) *v.sum = 0u;
-#endif
-}
-
-// Claim handed-over walks for the idle lanes (`idle`, wave-uniform).  Returns,
-// per lane, the claimed slot or 0xFFFFFFFF.  Own wave first (liveness), then
-// the waves the summary names.  Called by the whole wave (uniform control).
-template <uint32_t NT>
-__device__ __forceinline__ uint32_t pool_claim(const PoolView& v, uint32_t wave, bool own_first,
-                                               unsigned long long idle) {
-    uint32_t got = 0xFFFFFFFFu;
-#if defined(__HIP_DEVICE_COMPILE__)
-    constexpr uint32_t NW = NT / 64u;
-    uint32_t cand = __hip_atomic_load(v.sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    cand = wave_uniform(cand);
-    if (own_first) cand |= 1u << wave;
-    // rotate so the scan starts at this wave
-    cand = ((cand >> wave) | (cand << ((NW - wave) % NW))) & ((1u << NW) - 1u);
-    while (cand != 0u && idle != 0ull) {
-        const uint32_t k = (uint32_t)__builtin_ctz(cand);
-        cand &= cand - 1u;
-        const uint32_t w = (wave + k) % NW;
-        // take at most as many walks as there are idle lanes: the lowest bits
-        const uint32_t n_idle = (uint32_t)__popcll(idle);
-        unsigned long long want = ~0ull;
-        {
-            unsigned long long r = __hip_atomic_load(&v.ready[w], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-            r = ((unsigned long long)wave_uniform((uint32_t)(r >> 32)) << 32) | wave_uniform((uint32_t)r);
-            if (r == 0ull) continue;
-            want = r;
-            while ((uint32_t)__popcll(want) > n_idle) want &= ~(1ull << (63 - __builtin_clzll(want)));
-        }
-        unsigned long long old = 0ull;
-        if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-            old = __hip_atomic_fetch_and(&v.ready[w], ~want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        old = ((unsigned long long)wave_uniform((uint32_t)(old >> 32)) << 32) | wave_uniform((uint32_t)old);
-        unsigned long long cl = old & want;
-        if (old != 0ull && (old & ~want) == 0ull &&
-            __lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-            __hip_atomic_fetch_and(v.sum, ~(1u << w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // deal the claimed walks to idle lanes in order
-        while (cl != 0ull) {
-            const uint32_t s = (uint32_t)__builtin_ctzll(cl);
-            const uint32_t l = (uint32_t)__builtin_ctzll(idle);
-            cl &= cl - 1ull;
-            idle &= idle - 1ull;
-            got = (__lane_id() == l) ? w * 64u + s : got;
-        }
-    }
-#endif
-    return got;
-}
-
-template <bool ANY>
-__device__ __forceinline__ void sphere_walk_pool(const uint4* __restrict__ ent,
-                                                 const uint16_t* __restrict__ ids, uint32_t nN,
-                                                 uint32_t nT, uint8_t* pool_base, f3& o, f3& d,
-                                                 float& best, int& id) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    constexpr uint32_t NT = RT_SPH_BLOCK;
-    constexpr uint32_t kNone = 0xFFFFFFFFu, kClaimed = 0x10000u, kAnyBit = 0x20000u;
-#ifdef RT_TIMING_NO_SPH_WALK
-    return;
-#endif
-    const PoolView v = pool_view<NT>(pool_base);
-    // threadIdx.x through an opaque copy at each use: slot addresses hoisted
-    // out of the sample loop would hold VGPRs (and spill) for the whole launch
-    auto opaque_me = []() {
-        uint32_t t = threadIdx.x;
-        asm volatile("" : "+v"(t));
-        return t;
-    };
-    uint32_t me = opaque_me();
-    const uint32_t wave = wave_uniform(me >> 6);
-    const uint32_t lane = __lane_id();
-    // this lane's query in its slot: read back at the end, whoever walked it
-    v.a[me] = make_float4(o.x, o.y, o.z, best);
-    v.b[me] = make_float4(d.x, d.y, d.z, 0.0f);
-    float a = dot(d, d);
-    RayBox rb = ray_box(o, d);
-    uint32_t idx = octant(d) * nN;
-    uint32_t end = idx + nN;
-    if (ANY && id >= 0) idx = end;
-    uint32_t cur = me | (ANY ? kAnyBit : 0u);   // slot of the walk this lane runs (+ kind bits)
-    float pb = 0.0f, pdisc = 0.0f;               // parked leaf idx - 1 while pdisc > 0
-    unsigned long long handed = 0ull;            // wave-uniform: walks this wave handed over
-    bool over = false;                           // wave-uniform: handed over (once per query)
-    const int n_exec = __popcll(__builtin_amdgcn_ballot_w64(true));
-    int refill_at = 0;                           // wave-uniform
-    uint32_t guard = 0;                          // wave-uniform: polls while waiting
-    for (;;) {
-        for (;;) {  // cheap steps
-            const bool adv = idx < end && !(pdisc > 0.0f);
-            if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
-            if (adv) {
-                const uint4 e = ent[idx];
-                if (e.w & 0x80000000u) {
-                    idx = lds_node_hit(e, rb, 0.0f, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
-                } else {  // sph_test up to the discriminant (shaders_old.metal:108-136)
-                    const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y), __uint_as_float(e.z)};
-                    const float bq = 2.0f * dot(oc, d);
-                    const float cc = dot(oc, oc) - __uint_as_float(e.w);
-                    const float disc = bq * bq - (4.0f * a) * cc;
-                    if (disc > 0.0f) {
-                        pb = bq;
-                        pdisc = disc;
-                    }
-                    idx = idx + 1;
-                }
-            }
-            const int parked = __popcll(__builtin_amdgcn_ballot_w64(pdisc > 0.0f));
-            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || pdisc > 0.0f));
-            if (RT_SPH_PARK_DEN * parked >= live) break;
-            if (!over ? live <= RT_SPH_POOL_T : n_exec - live >= refill_at) break;
-        }
-        if (__builtin_amdgcn_ballot_w64(pdisc > 0.0f) != 0) {  // roots of the parked leaves
-            if (pdisc > 0.0f) {
-                const bool any = (cur & kAnyBit) != 0u;
-                const float tmin = any ? 0.0f : 1e-3f;
-                const float sq = sqrtf(pdisc);
-                const float a2 = 2.0f * a;
-                float t = (-pb - sq) / a2;
-                if (!(t > tmin)) t = (-pb + sq) / a2;
-                if (any) {
-                    if (t > tmin && t < best) {
-                        id = 0;
-                        idx = end;
-                    }
-                } else if (t > tmin && t < 3.0e38f && t <= best) {
-                    const int s = (int)(nT + ids[idx - 1u]);
-                    if (t < best || s < id) {
-                        best = t;
-                        id = s;
-                    }
-                }
-                pdisc = 0.0f;
-            }
-        }
-        // finished walks: the result to the query's slot (claimed: + the owner's done bit)
-        const bool fin = cur != kNone && idx >= end;
-        if (fin) {
-            const uint32_t s = cur & 0xFFFFu;
-            ((lds_f32_t*)&v.a[s])[3] = best;
-            v.c[s] = (uint32_t)(id + 1);
-        }
-        if (__builtin_amdgcn_ballot_w64(fin && (cur & kClaimed)) != 0ull) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (fin && (cur & kClaimed))
-                __hip_atomic_fetch_or(&v.done[(cur & 0xFFFFu) >> 6], 1ull << (cur & 63u), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (fin) {
-            cur = kNone;
-            idx = end = 0u;
-        }
-        // hand over this wave's last walks (all of them are its own until now)
-        if (!over) {
-            const unsigned long long give = __builtin_amdgcn_ballot_w64(cur != kNone);
-            if (__popcll(give) <= RT_SPH_POOL_T) {
-                over = true;
-                handed = give;
-                if (give != 0ull) {
-                    if (cur != kNone) {
-                        me = cur & 0xFFFFu;  // (own walks only before the hand-over)
-                        ((lds_f32_t*)&v.a[me])[3] = best;
-                        ((lds_u32_t*)&v.b[me])[3] = idx;
-                        v.c[me] = (uint32_t)(id + 1) | ((cur & kAnyBit) ? 0x80000000u : 0u);
-                        cur = kNone;
-                        idx = end = 0u;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) {
-                        __hip_atomic_fetch_or(&v.ready[wave], give, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(v.sum, 1u << wave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-            }
-        }
-        if (!over) continue;
-        // idle lanes claim handed-over walks (this wave's first)
-        const unsigned long long idle = __builtin_amdgcn_ballot_w64(cur == kNone);
-        bool waiting = false;
-        if (idle != 0ull) {
-            const uint32_t got = pool_claim<NT>(v, wave, handed != 0ull, idle);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (got != kNone) {
-                const float4 qa = v.a[got], qb = v.b[got];
-                const uint32_t qc = v.c[got];
-                o = f3{qa.x, qa.y, qa.z};
-                best = qa.w;
-                d = f3{qb.x, qb.y, qb.z};
-                idx = __float_as_uint(qb.w);
-                id = (int)(qc & 0x7FFFFFFFu) - 1;
-                cur = got | kClaimed | ((qc >> 31) ? kAnyBit : 0u);
-                a = dot(d, d);
-                rb = ray_box(o, d);
-                end = (octant(d) + 1u) * nN;
-            }
-            refill_at = n_exec - __popcll(__builtin_amdgcn_ballot_w64(idx < end)) + RT_SPH_POOL_REFILL;
-        }
-        if (__builtin_amdgcn_ballot_w64(cur != kNone) == 0ull) {
-            // nothing to walk: done once every handed-over walk of this wave is back
-            unsigned long long dn = __hip_atomic_load(&v.done[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            dn = ((unsigned long long)wave_uniform((uint32_t)(dn >> 32)) << 32) | wave_uniform((uint32_t)dn);
-            if ((dn & handed) == handed) break;
-            waiting = true;
-        }
-        if (waiting) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++guard > (1u << 18)) {  // liveness guard (never expected): poison the result
-                best = __uint_as_float(0x7FC00000u);
-                break;
-            }
-        }
-    }
-    if (handed != 0ull && lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-        __hip_atomic_fetch_and(&v.done[wave], ~handed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    me = opaque_me();
-    const float4 qa = v.a[me], qb = v.b[me];
-    const uint32_t qc = v.c[me];
-    const float b0 = best;
-    o = f3{qa.x, qa.y, qa.z};
-    d = f3{qb.x, qb.y, qb.z};
-    best = (b0 != b0) ? b0 : qa.w;
-    id = (int)(qc & 0x7FFFFFFFu) - 1;
-#endif
-}
-
-template <bool PACKET>
-__device__ __forceinline__ bool sphere_any_lds(const uint4* ent, uint32_t nN, f3 o, f3 d,
-                                               float tmin, float tmax) {
-    const float a = dot(d, d);
-    const RayBox rb = ray_box(o, d);
-    const uint32_t lay = PACKET ? wave_uniform(sph_layout(d)) : sph_layout(d);
-    bool found = false;
-    uint32_t idx = lay * nN;
-    const uint32_t end = idx + nN;
-    while (idx < end) {
-        const uint4 e = ent[idx];
-        uint32_t next = idx + 1;
-        if (e.w & 0x80000000u) {
-            const bool h = !found && lds_node_hit(e, rb, tmin, tmax);
-            if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) next = e.w & 0x7FFFFFFFu;
-        } else {
-            float t;
-            found = found || sph_test(make_float4(__uint_as_float(e.x), __uint_as_float(e.y),
-                                                  __uint_as_float(e.z), __uint_as_float(e.w)),
-                                      o, d, a, tmin, tmax, &t);
-            if (!PACKET && found) return true;
-            if (PACKET && __builtin_amdgcn_ballot_w64(!found) == 0) break;
-        }
-        idx = PACKET ? wave_uniform(next) : next;
-    }
-    return found;
-}
-
-// Triangle-BVH walks: the sphere walks above with the triangle test in the
-// leaves (one triangle per leaf) — same conservative boxes, same (t, id)
-// ranking, so the result is the id-ordered brute-force scan's.
-template <bool PACKET>
-__device__ __forceinline__ void tri_bvh_closest(const float4* __restrict__ node,
-                                                const float4* __restrict__ tri,
-                                                const uint32_t* __restrict__ perm, uint32_t nN,
-                                                f3 o, f3 d, float tmin, float& best, int& id) {
-    const RayBox rb = ray_box(o, d);
-    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
-    uint32_t idx = 0;
-    while (idx < nN) {
-        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
-        uint32_t next = PACKET ? wave_uniform(__float_as_uint(n0.w)) : __float_as_uint(n0.w);
-        const bool h = node_hit(n0, n1, rb, tmin, best);
-        if (PACKET ? __builtin_amdgcn_ballot_w64(h) != 0 : h) {
-            const uint32_t leaf = PACKET ? wave_uniform(__float_as_uint(n1.w)) : __float_as_uint(n1.w);
-            if (leaf == 0u) {
-                next = idx + 1;
-            } else {
-                const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                for (uint32_t k = first; k < end; ++k) {
-                    float t;
-                    if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f,
-                                 &t) && t <= best) {
-                        const int tid = (int)perm[k];
-                        if (t < best || tid < id) {
-                            best = t;
-                            id = tid;
-                        }
-                    }
-                }
-            }
-        }
-        idx = next;
-    }
-}
-
-template <bool PACKET>
-__device__ __forceinline__ bool tri_bvh_any(const float4* __restrict__ node,
-                                            const float4* __restrict__ tri, uint32_t nN, f3 o,
-                                            f3 d, float tmin, float tmax) {
-    const RayBox rb = ray_box(o, d);
-    node += 2u * nN * (PACKET ? wave_uniform(octant(d)) : octant(d));
-    bool found = false;
-    uint32_t idx = 0;
-    while (idx < nN) {
-        const float4 n0 = node[2 * idx], n1 = node[2 * idx + 1];
-        if (PACKET) {
-            uint32_t next = wave_uniform(__float_as_uint(n0.w));
-            if (__builtin_amdgcn_ballot_w64(!found && node_hit(n0, n1, rb, tmin, tmax)) != 0) {
-                const uint32_t leaf = wave_uniform(__float_as_uint(n1.w));
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        found = found || tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d,
-                                                  tmin, tmax, &t);
-                    }
-                    if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
-                }
-            }
-            idx = next;
-        } else {
-            uint32_t next = __float_as_uint(n0.w);
-            if (node_hit(n0, n1, rb, tmin, tmax)) {
-                const uint32_t leaf = __float_as_uint(n1.w);
-                if (leaf == 0u) {
-                    next = idx + 1;
-                } else {
-                    const uint32_t first = leaf & 0xFFFFFFu, end = first + (leaf >> 24);
-                    for (uint32_t k = first; k < end; ++k) {
-                        float t;
-                        if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax,
-                                     &t))
-                            return true;
-                    }
-                }
-            }
-            idx = next;
-        }
-    }
-    return found;
 }
 
 // Triangle-BVH walks over the compact entries (rt_lbvh.hip: 16 B per node, fp16
-// boxes rounded outward, two layouts -- near child first for (+,+,+) and for
-// (-,-,-), a ray takes the one matching most of its direction signs -- stored
-// after the 8 full layouts): the same stackless depth-first walks, conservative
-// boxes and (t, id) ranking as tri_bvh_*, with half the bytes per step and a
-// quarter of the layouts in the caches.
+// boxes rounded outward, one layout per direction octant, near child first,
+// stored after the 8 full 32-B layouts): stackless depth-first walks with
+// conservative boxes and (t, id) ranking.
 __device__ __forceinline__ const uint4* tri_compact(const float4* node, uint32_t nN) {
     return reinterpret_cast<const uint4*>(node + 16u * nN);
 }
-__device__ __forceinline__ uint32_t tri_compact_layout(f3 d) {
-    return RT_TRI_COMPACT_LAYOUTS == 8 ? octant(d) : lds_layout(d);
-}
 
-template <bool PACKET>
-__device__ __forceinline__ void tri_cbvh_closest(const uint4* __restrict__ cn,
-                                                 const float4* __restrict__ tri,
-                                                 const uint32_t* __restrict__ perm, uint32_t nN,
-                                                 f3 o, f3 d, float tmin, float& best, int& id) {
+// Wave-packet walks for the coherent camera rays and bounce-0 shadow rays: the
+// wave walks ONE path (the layout of its first lane's octant) and enters a node
+// when any lane's box test passes; the node index is wave uniform.  A lane whose
+// own test failed still tests the leaf's triangle, which cannot change its result.
+__device__ __forceinline__ void tri_cbvh_closest_packet(const uint4* __restrict__ cn,
+                                                        const float4* __restrict__ tri,
+                                                        const uint32_t* __restrict__ perm, uint32_t nN,
+                                                        f3 o, f3 d, float tmin, float& best, int& id) {
     const RayBox rb = ray_box(o, d);
-    uint32_t idx = (PACKET ? wave_uniform(tri_compact_layout(d)) : tri_compact_layout(d)) * nN;
+    uint32_t idx = wave_uniform(octant(d)) * nN;
     const uint32_t end = idx + nN;
     while (idx < end) {
         const uint4 e = cn[idx];
-        const bool inner = (e.w & 0x80000000u) != 0u;  // wave-uniform for PACKET
+        const bool inner = (e.w & 0x80000000u) != 0u;  // wave-uniform
         const bool h = lds_node_hit(e, rb, tmin, best);
         uint32_t next = idx + 1;
-        if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) {
+        if (__builtin_amdgcn_ballot_w64(h) == 0) {
             if (inner) next = e.w & 0x7FFFFFFFu;
         } else if (!inner) {
             const uint32_t k = e.w;
@@ -1116,15 +454,15 @@ __device__ __forceinline__ void tri_cbvh_closest(const uint4* __restrict__ cn,
                 }
             }
         }
-        idx = PACKET ? wave_uniform(next) : next;
+        idx = wave_uniform(next);
     }
 }
 
-template <bool PACKET>
-__device__ __forceinline__ bool tri_cbvh_any(const uint4* __restrict__ cn, const float4* __restrict__ tri,
-                                             uint32_t nN, f3 o, f3 d, float tmin, float tmax) {
+__device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn,
+                                                    const float4* __restrict__ tri, uint32_t nN, f3 o,
+                                                    f3 d, float tmin, float tmax) {
     const RayBox rb = ray_box(o, d);
-    uint32_t idx = (PACKET ? wave_uniform(tri_compact_layout(d)) : tri_compact_layout(d)) * nN;
+    uint32_t idx = wave_uniform(octant(d)) * nN;
     const uint32_t end = idx + nN;
     bool found = false;
     while (idx < end) {
@@ -1132,37 +470,36 @@ __device__ __forceinline__ bool tri_cbvh_any(const uint4* __restrict__ cn, const
         const bool inner = (e.w & 0x80000000u) != 0u;
         const bool h = !found && lds_node_hit(e, rb, tmin, tmax);
         uint32_t next = idx + 1;
-        if (PACKET ? __builtin_amdgcn_ballot_w64(h) == 0 : !h) {
+        if (__builtin_amdgcn_ballot_w64(h) == 0) {
             if (inner) next = e.w & 0x7FFFFFFFu;
         } else if (!inner) {
             const uint32_t k = e.w;
             float t;
             found = found || tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax, &t);
-            if (!PACKET && found) return true;
-            if (PACKET && __builtin_amdgcn_ballot_w64(!found) == 0) break;
+            if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
         }
-        idx = PACKET ? wave_uniform(next) : next;
+        idx = wave_uniform(next);
     }
     return found;
 }
 
-// Per-lane compact-BVH walks with POSTPONED LEAVES (as sphere_walk_lds parks
-// its roots): a lane whose box test passes at a leaf parks the triangle and
-// stops; the others walk on until at least half of the lanes still walking
-// are parked, then the wave runs the triangle tests of all parked lanes
-// together -- instead of every mixed step paying for the box test AND the
-// three record loads and the test of a triangle.  Per lane the entries are
-// visited in the same order and ranked by (t, id): the same result.
-#ifndef RT_TRI_PARK_DEN
-#define RT_TRI_PARK_DEN 4  // the parked leaves are tested once they are >= 1/DEN of the live lanes
-#endif
+// Per-lane compact-BVH walks with POSTPONED LEAVES (as sphere_walk parks its
+// roots): a lane whose box test passes at a leaf parks the triangle and
+// stops; the others walk on until at least 1/kTriParkDen of the lanes
+// still walking are parked, then the wave runs the triangle tests of all
+// parked lanes together -- instead of every mixed step paying for the box
+// test AND the three record loads and the test of a triangle.  Per lane the
+// entries are visited in the same order and ranked by (t, id): the same result.
+// the parked leaves are tested once they are >= 1/kTriParkDen of the live lanes
+// (100k triangles: 1/4 738, 1/2 701, 3/4 570, 1/8 707 Msamples/s)
+constexpr int kTriParkDen = 4;
 template <bool ANY>
 __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, const float4* __restrict__ tri,
                                               const uint32_t* __restrict__ perm, uint32_t nN, f3 o, f3 d,
                                               float tmin, float& best, int& id) {
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     const RayBox rb = ray_box(o, d);
-    uint32_t idx = tri_compact_layout(d) * nN;
+    uint32_t idx = octant(d) * nN;
     const uint32_t end = idx + nN;
     if (ANY && id >= 0) idx = end;
     uint32_t leaf = kNone;
@@ -1182,7 +519,7 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
             }
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
-            if (RT_TRI_PARK_DEN * parked >= live) break;
+            if (kTriParkDen * parked >= live) break;
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
         if (leaf != kNone) {
@@ -1204,17 +541,6 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
         }
     }
 }
-
-#ifndef RT_TRI_PARK
-#define RT_TRI_PARK 1  // per-lane triangle-BVH walks with postponed leaves (tri_cbvh_walk)
-#endif
-#ifndef RT_TRI_PARK_ALL
-#define RT_TRI_PARK_ALL 0  // 1: also camera and bounce-0 shadow rays (else wave-packet walks)
-#endif
-
-#ifndef RT_TRI_COMPACT
-#define RT_TRI_COMPACT 1  // triangle-BVH walks over the compact 16-B entries
-#endif
 
 // ---- box clusters ------------------------------------------
 // Candidate pairs of one ray among the clustered pairs: bit k set when pair k
@@ -1292,9 +618,7 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
         const float tlo0 = vmax3(en[0], en[1], vmax(en[2], tmin));
         const float thi0 = vmin3(ex[0], ex[1], vmin(ex[2], tmax));
         const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
-#ifndef RT_NO_CLU_WAVE_SKIP
         if (!__builtin_amdgcn_ballot_w64(tlo <= thi)) continue;  // no lane meets the box
-#endif
         const uint32_t m[6] = {__float_as_uint(M0.x), __float_as_uint(M0.y), __float_as_uint(M0.z),
                                __float_as_uint(M0.w), __float_as_uint(M1.x), __float_as_uint(M1.y)};
         uint32_t cm = 0;
@@ -1400,8 +724,6 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
 // With CULL (used for coherent camera rays) a pair is skipped when no lane's
 // box around its current candidate segment [o, o + d*best] touches the pair's
 // padded AABB: any hit that could still win has t < best and lies inside it.
-// o and d are references so that the pooled sphere walk (which hands them
-// back bit-identical) does not make the caller keep a second copy live.
 template <int GEO, bool SPH, bool CULL, int QT = 0>
 __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, float tmin,
                                            float* t_io) {
@@ -1456,14 +778,13 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, fl
             }
         }
     } else if (GEO == kGeoTriBvh) {
-        if (RT_TRI_COMPACT && RT_TRI_PARK && (!CULL || RT_TRI_PARK_ALL))
+        // camera rays: wave packets; bounce rays: per-lane walks with parked leaves
+        if (CULL)
+            tri_cbvh_closest_packet(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+                                    best, id);
+        else
             tri_cbvh_walk<false>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                  best, id);
-        else if (RT_TRI_COMPACT)
-            tri_cbvh_closest<CULL>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d,
-                                   tmin, best, id);
-        else
-            tri_bvh_closest<CULL>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin, best, id);
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
             float t;
@@ -1474,15 +795,10 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, fl
             }
         }
     }
-    if (SPH && GEO == kGeoSphLds && ((CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3))
-        sphere_closest_lds<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
-    else if (SPH && GEO == kGeoSphLds && RT_SPH_POOL)
-        sphere_walk_pool<false>(sv.sent, sv.sid, sv.nN, sv.nT, sv.pool, o, d, best, id);
-    else if (SPH && GEO == kGeoSphLds)
-        sphere_walk_lds<false, RT_SPH_SPLIT != 0>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id,
-                                                  sv.wscr);
+    if (SPH && GEO == kGeoSphLds)
+        sphere_walk<false>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
     else if (SPH)
-        sphere_closest<(CULL && RT_SPH_PACKET) || RT_SPH_PACKET >= 3>(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
+        sphere_closest(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
     *t_io = best;
     return id;
 }
@@ -1526,16 +842,15 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float
             }
         }
     } else if (GEO == kGeoTriBvh) {
-        if (RT_TRI_COMPACT && RT_TRI_PARK && (!PACKET || RT_TRI_PARK_ALL)) {
+        if (PACKET) {  // bounce-0 shadow rays: wave packets
+            if (tri_cbvh_any_packet(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o, d, tmin, tmax))
+                return true;
+        } else {
             float tm = tmax;
             int hid = -1;
             tri_cbvh_walk<true>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                 tm, hid);
             if (hid >= 0) return true;
-        } else if (RT_TRI_COMPACT ? tri_cbvh_any<PACKET>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o,
-                                                         d, tmin, tmax)
-                                  : tri_bvh_any<PACKET>(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax)) {
-            return true;
         }
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
@@ -1545,21 +860,13 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float
                 return true;
         }
     }
-    if (SPH && GEO == kGeoSphLds && PACKET) return sphere_any_lds<true>(sv.sent, sv.nN, o, d, tmin, tmax);
-    if (SPH && GEO == kGeoSphLds && RT_SPH_POOL) {
-        float tm = tmax;
-        int id = -1;
-        sphere_walk_pool<true>(sv.sent, sv.sid, sv.nN, sv.nT, sv.pool, o, d, tm, id);
-        return id >= 0;
-    }
     if (SPH && GEO == kGeoSphLds) {
         float tm = tmax;
         int id = -1;
-        sphere_walk_lds<true, RT_SPH_SPLIT != 0 && !RT_SPH_SPLIT_CLOSEST_ONLY>(
-            sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id, sv.wscr);
+        sphere_walk<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id);
         return id >= 0;
     }
-    if (SPH) return sphere_any<PACKET>(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
+    if (SPH) return sphere_any(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
     return false;
 }
 
@@ -1622,76 +929,6 @@ __device__ __forceinline__ FusedHit fused_shadow_closest(const SceneView& sv, f3
             }
         }
     }
-    return h;
-}
-
-// Fused shadow any-hit of bounce b and closest hit of bounce b+1 over the box
-// clusters (kGeoPairClu; the cluster twin of fused_shadow_closest): both rays
-// start at p, so after both candidate masks are formed each lane tests ONE
-// candidate pair per round -- a shadow candidate while its shadow ray is not yet
-// occluded, else a closest candidate -- instead of running the shadow rounds
-// and then the closest rounds each to the wave's longest list.  Every test is
-// pair_test_rank's (same arithmetic, same (t, id) ranking, candidates visited
-// out of id order as there), so each lane's two results are exactly those of
-// cluster_query<true> and cluster_query<false>.
-__device__ __forceinline__ FusedHit fused_cluster_query(const SceneView& sv, f3 p, f3 L, float smax,
-                                                        f3 d2) {
-    FusedHit h{false, -1, 1000.0f};  // max_distance (sampling.metal:155)
-    float tm = smax;
-    int sid = -1;
-    for (uint32_t free = sv.pair_free; free != 0u; free &= free - 1u) {
-        const uint32_t k = (uint32_t)__builtin_ctz(free);
-        pair_test_rank<true>(sv.pair + kPairF4 * k, k, p, L, 0.0f, &tm, &sid);
-        pair_test_rank<false>(sv.pair + kPairF4 * k, k, p, d2, 0.001f, &h.t, &h.id);
-    }
-    uint32_t cs = sid >= 0 ? 0u : cluster_candidates<true>(sv, p, L, 0.0f, smax);
-    uint32_t cc = cluster_candidates<false>(sv, p, d2, 0.001f, h.t);
-    while ((cs | cc) != 0u) {
-        const bool shadow = cs != 0u;
-        const uint32_t k = (uint32_t)__builtin_ctz(shadow ? cs : cc);
-        if (shadow)
-            cs &= cs - 1u;
-        else
-            cc &= cc - 1u;
-        // pair_test_rank with the mode chosen per lane
-        const f3 dir = shadow ? L : d2;
-        const float tmin = shadow ? 0.0f : 0.001f;
-        const float4* rr = sv.pair + kPairF4 * k;
-        const float4 r0 = rr[0], r1 = rr[1], r2 = rr[2], r3 = rr[3], r4 = rr[4];
-        const PairDots q = pair_dots(r0, r1, r2, r3, r4, p, dir);
-        const bool pa = bary_ok(q.denA, q.a1, q.a2);
-        const bool pb = bary_ok(q.denB, q.b1, q.b2);
-        if (pa || pb) {
-            const float best = shadow ? smax : h.t;
-            const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
-            const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
-            const int ia = (int)(pa ? 2 * k : 2 * k + 1);
-            bool hit = t > tmin && (t < best || (!shadow && t == best && ia < h.id));
-            float tb = t;
-            int ib = ia;
-            if (pa && pb) {
-                const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
-                const int i2 = (int)(2 * k + 1);
-                const float best2 = hit ? tb : best;
-                const int id2 = hit ? ib : h.id;
-                if (t2 > tmin && (t2 < best2 || (!shadow && t2 == best2 && i2 < id2))) {
-                    hit = true;
-                    tb = t2;
-                    ib = i2;
-                }
-            }
-            if (hit) {
-                if (shadow) {
-                    h.occluded = true;
-                    cs = 0u;  // any hit ends the shadow query (cluster_query<true>)
-                } else {
-                    h.t = tb;
-                    h.id = ib;
-                }
-            }
-        }
-    }
-    h.occluded = h.occluded || sid >= 0;
     return h;
 }
 

@@ -278,7 +278,7 @@ typedef struct rt_scene_info {
     uint32_t n_triangle_bvh_nodes; /* GPU-built triangle BVH nodes per layout (0: LDS layouts) */
     uint32_t n_box_clusters;     /* pair runs on the faces of one oriented box (slab-tested first) */
     uint32_t pair_free_mask;     /* pairs in no box cluster (bit k = pair k) */
-    uint32_t sphere_bvh_lds_bytes; /* compact sphere BVH staged in LDS (0: read from global) */
+    uint32_t sphere_kernel_lds_bytes; /* dynamic LDS of the sphere kernel (its pair records; 0: sphere kernel not taken) */
 } rt_scene_info;
 int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
 

@@ -79,7 +79,7 @@ def test_scene_layout_uses_shared_edge_pairs():
     # four box clusters: the room (5 walls), the two rotated boxes, the light rectangle
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
                     "lds_bytes": 18 * 112 + 4 * 112, "n_sphere_nodes": 0, "n_triangle_bvh_nodes": 0,
-                    "n_box_clusters": 4, "pair_free_mask": 0, "sphere_bvh_lds_bytes": 0}
+                    "n_box_clusters": 4, "pair_free_mask": 0, "sphere_kernel_lds_bytes": 0}
     boxes = g.Scene.random_boxes(16, 8, 4, seed=1).describe()
     assert boxes["n_box_clusters"] == 6 and boxes["pair_free_mask"] == 0  # room, 4 boxes, light
     soup = g.Scene.random_triangles(16, 8, 1000).describe()
@@ -98,9 +98,9 @@ def test_scene_layout_uses_shared_edge_pairs():
     # the compact sphere BVH (8 octant layouts x 1999 entries x 16 B, near/far
     # fp16 boxes) is read from global memory (L2): the compact-BVH kernel
     # stages only the pairs
-    assert info["sphere_bvh_lds_bytes"] == 6 * 112
+    assert info["sphere_kernel_lds_bytes"] == 6 * 112
     big = g.Scene.random_spheres(16, 8, 5000).describe()
-    assert big["lds_bytes"] == 6 * 112 and big["sphere_bvh_lds_bytes"] == 6 * 112
+    assert big["lds_bytes"] == 6 * 112 and big["sphere_kernel_lds_bytes"] == 6 * 112
     assert big["n_sphere_nodes"] == bvh_nodes(5000)
 
 

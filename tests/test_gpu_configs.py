@@ -198,7 +198,7 @@ def test_c4_timed_launch_1080p_256spp_bands_vs_oracle():
     assert info["kernel"] == C4_KERNEL, info
     assert info["lanes_per_pixel"] == 16 and info["block_threads"] == C4_BLOCK, info
     assert (info["grid_x"], info["grid_y"]) == C4_GRID, info
-    assert info["lds_bytes"] == s.describe()["sphere_bvh_lds_bytes"], info
+    assert info["lds_bytes"] == s.describe()["sphere_kernel_lds_bytes"], info
     assert np.isfinite(frame).all() and np.all(frame[..., 3] == 1.0)
     for start in (100, 540, 900):
         ref = oracle_lib.render(s, sd, 256, 3, row_start=start, row_count=4, threads=16)

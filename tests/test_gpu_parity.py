@@ -146,7 +146,7 @@ def test_sphere_bvh_lds_fp16_boxes_far_spheres():
         sp.center.x, sp.center.y, sp.center.z = (sp.center.x * 2900.0, sp.center.y * 2900.0,
                                                  -abs(sp.center.z) * 2900.0 - 50.0)
         sp.radius = sp.radius * 2900.0
-    assert s.describe()["sphere_bvh_lds_bytes"] > 0
+    assert s.describe()["sphere_kernel_lds_bytes"] > 0
     sd = seed_splitmix(40, 24, key=17)
     with Renderer(s, seeds=sd) as r:
         out = r.render(RenderParams(spp=2, bounces=3))
