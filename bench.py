@@ -328,10 +328,18 @@ def main(argv=None, backend_factory=CudaBackend):
         kernel_ms, basis = step_ms, "whole step: every progressive launch + the gather (HIP events)"
     else:
         kernel_ms, basis = renderer.last_kernel_ms(), "the render launch of the last step (HIP events)"
+    # the gather's share of a step on this rank: the step minus its render
+    # launch (not separable in progressive mode, where the C-ABI runs several
+    # launches and the gather inside one call)
+    gather_ms = step_ms - kernel_ms if world > 1 and not args.batch_spp else None
+    per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms, step_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms_max, step_ms_max = (float(v) for v in t)
+        mine = torch.tensor([elapsed, kernel_ms, step_ms, -1.0 if gather_ms is None else gather_ms],
+                            dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = torch.stack(allr).numpy()
+        elapsed, kernel_ms_max, step_ms_max = (float(v) for v in per_rank[:, :3].max(axis=0))
     else:
         kernel_ms_max, step_ms_max = kernel_ms, step_ms
 
@@ -412,6 +420,14 @@ def main(argv=None, backend_factory=CudaBackend):
         if comm is not None:
             out.update(comm)
             out["gather_check"] = gather_check
+            # render imbalance vs collective: the slowest and fastest render
+            # launch over the ranks, and the gather's share of each rank's step
+            out["kernel_ms_min_rank"] = round(float(per_rank[:, 1].min()), 4)
+            out["gather_ms"] = (None if gather_ms is None else
+                                round(float(per_rank[:, 3].max()), 4))
+            out["gather_ms_basis"] = ("step - render launch on each rank (HIP events), max over ranks"
+                                      if gather_ms is not None else
+                                      "not separable: progressive launches and the gather run in one call")
         if world == 1 and args.cpu_baseline != "off":
             # every CPU this process may run on at once: the affinity mask,
             # capped by the cgroup CPU quota (oversubscribing a 16-CPU quota
