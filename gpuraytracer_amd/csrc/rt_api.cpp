@@ -32,9 +32,6 @@ struct rt_ctx {
     float4* d_clusters = nullptr;
     uint32_t* d_sph_lds = nullptr;
     uint16_t* d_sph_lds_id = nullptr;
-    uint32_t* d_sph_wide = nullptr;
-    uint32_t* d_sph_wide_id = nullptr;
-    bool sph_binary = false;  // RTPT_SPH_WALK=binary: the compact binary sphere BVH instead of the 4-wide one
     float4* d_sph_isect = nullptr;
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
@@ -125,8 +122,6 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_clusters);
     (void)hipFree(c->d_sph_lds);
     (void)hipFree(c->d_sph_lds_id);
-    (void)hipFree(c->d_sph_wide);
-    (void)hipFree(c->d_sph_wide_id);
     (void)hipFree(c->d_sph_isect);
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_sph_nodes);
@@ -231,10 +226,6 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.sph_isect = c->d_sph_isect;
     K.sph_lds = c->scene.sph_lds.empty() ? nullptr : c->d_sph_lds;
     K.sph_lds_id = c->d_sph_lds_id;
-    const bool wide = !c->scene.sph_wide.empty() && !c->sph_binary;
-    K.sph_wide = wide ? reinterpret_cast<const uint4*>(c->d_sph_wide) : nullptr;
-    K.sph_wide_id = c->d_sph_wide_id;
-    K.sph_wide_stack = wide ? c->scene.sph_wide_stack : 0u;
     K.sph_shade = c->d_sph_shade;
     K.sph_nodes = c->d_sph_nodes;
     K.sph_perm = c->d_sph_perm;
@@ -603,7 +594,6 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
     c->device = d->device;
     if (const char* m = getenv("RTPT_LANES")) c->lanes = (uint32_t)atoi(m);
-    if (const char* m = getenv("RTPT_SPH_WALK")) c->sph_binary = !strcmp(m, "binary");  // tuning knob
     if (const char* m = getenv("RTPT_SCENE_MEM")) {
         if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
@@ -636,8 +626,6 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
             (e = upload(&c->d_clusters, s.clusters.data(), s.clusters.size() * sizeof(float), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_lds, s.sph_lds.data(), s.sph_lds.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_lds_id, s.sph_lds_id.data(), s.sph_lds_id.size() * sizeof(uint16_t), c->stream)) != hipSuccess ||
-            (e = upload(&c->d_sph_wide, s.sph_wide.data(), s.sph_wide.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
-            (e = upload(&c->d_sph_wide_id, s.sph_wide_id.data(), s.sph_wide_id.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_nodes, s.sph_nodes.data(), s.sph_nodes.size() * sizeof(rt::BvhNode), c->stream)) != hipSuccess ||

@@ -384,7 +384,7 @@ constexpr int kMinWavesPerEuClu = 7;
 // kernel at 128 / 64 / 512 threads ran 40.1 / 68.9 / 27.8 ms vs 26.2 (its 22 KB
 // of Halton tables per workgroup then cap the waves per CU), the
 // triangle-BVH kernel at 64 / 128 threads 204.3 / 192.1 ms vs 180.7.
-constexpr uint32_t block_threads(int geo) { return geo_sph_kernel(geo) ? kSphBlockThreads : kBlockThreads; }
+constexpr uint32_t block_threads(int geo) { return geo == kGeoSphLds ? kSphBlockThreads : kBlockThreads; }
 constexpr uint32_t waves_per_row(int geo) { return block_threads(geo) >= 128 ? 2u : 1u; }
 constexpr uint32_t waves_per_col(int geo) { return block_threads(geo) / 64u / waves_per_row(geo); }
 
@@ -404,18 +404,13 @@ void path_trace_kernel(KParams P) {
         sv.pair = P.pair_isect;
     } else if (GEO != kGeoTriGlobal) {
         // Stage the intersection records once per workgroup.
-        constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu || geo_sph_kernel(GEO);
+        constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu || GEO == kGeoSphLds;
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
         if (GEO == kGeoSphLds) {  // the compact sphere BVH (8 layouts) stays in global memory (L2)
             sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
             sv.sid = P.sph_lds_id;
-        }
-        if (GEO == kGeoSphWide) {  // the 4-wide BVH in global memory (L2), the walk stacks after the pairs
-            sv.swide = P.sph_wide;
-            sv.swid = P.sph_wide_id;
-            sv.stk = (__attribute__((address_space(3))) uint16_t*)(lds + ng4);
         }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
@@ -481,7 +476,7 @@ void path_trace_kernel(KParams P) {
     // Only for the box-cluster and LDS-sphere kernels: the triangle-BVH walk
     // kernel (global-memory nodes) ran 16 % slower with the opaque copies
     // (325 vs 281 ms, 10k triangles) and spills about as much without them.
-    constexpr bool kRemat = GEO == kGeoPairClu || geo_sph_kernel(GEO);
+    constexpr bool kRemat = GEO == kGeoPairClu || GEO == kGeoSphLds;
     auto opaque_tid = []() {
         uint32_t t = threadIdx.x;
         if constexpr (kRemat) asm volatile("" : "+v"(t));
@@ -737,7 +732,7 @@ inline int lanes_per_pixel(const KParams& P, int geo) {
     // of N = 8 19,450 vs 18,824); whole frames of >= 1 M pixels keep 4 (1080p
     // 20,288 vs 20,143; 4096^2 18,505 vs 17,978)
     const bool share16 = P.row_step > 1 && P.spp >= 16u * kHaltonTabMinRounds;
-    const int want = (px >= 1000000ull && !geo_sph_kernel(geo) && !share16) ? 4 : 16;
+    const int want = (px >= 1000000ull && geo != kGeoSphLds && !share16) ? 4 : 16;
     if (P.spp >= (uint32_t)want) return want;
     return P.spp >= 4 ? 4 : 1;
 }
@@ -777,7 +772,7 @@ hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     constexpr uint32_t WR = waves_per_row(GEO), WC = waves_per_col(GEO);
     const uint32_t TX = WR * Q.wave_w, TY = WC * ((64u / L) / Q.wave_w);
     const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);
-    if (geo_sph_kernel(GEO)) {
+    if (GEO == kGeoSphLds) {
         const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL, L>, lds_bytes);
         if (e != hipSuccess) return e;
     }
@@ -797,7 +792,7 @@ hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     }
     constexpr uint32_t TX = 8u * waves_per_row(GEO), TY = 8u * waves_per_col(GEO);  // 8x8-pixel waves
     const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);
-    if (geo_sph_kernel(GEO)) {
+    if (GEO == kGeoSphLds) {
         const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL>, lds_bytes);
         if (e != hipSuccess) return e;
     }
@@ -814,7 +809,7 @@ hipError_t launch_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     if constexpr (GEO == kGeoPairClu)  // triangle-only scenes (launch_path_trace)
         return small ? launch_t<B, GEO, false, true>(P, lds_bytes, stream)
                      : launch_t<B, GEO, false, false>(P, lds_bytes, stream);
-    if constexpr (geo_sph_kernel(GEO))  // sphere scenes only
+    if constexpr (GEO == kGeoSphLds)  // sphere scenes only
         return small ? launch_t<B, GEO, true, true>(P, lds_bytes, stream)
                      : launch_t<B, GEO, true, false>(P, lds_bytes, stream);
     if (P.nS > 0)
@@ -849,7 +844,6 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
         case kGeoPairLds: return launch_g<B, kGeoPairLds>(P, lds_bytes, stream);
         case kGeoPairClu: return launch_g<B, kGeoPairClu>(P, lds_bytes, stream);
         case kGeoSphLds: return launch_g<B, kGeoSphLds>(P, lds_bytes, stream);
-        case kGeoSphWide: return launch_g<B, kGeoSphWide>(P, lds_bytes, stream);
         case kGeoPairSmem: return launch_g<B, kGeoPairSmem>(P, lds_bytes, stream);
         case kGeoTriBvh: return launch_g<B, kGeoTriBvh>(P, lds_bytes, stream);
         case kGeoTriLds: return launch_g<B, kGeoTriLds>(P, lds_bytes, stream);
@@ -880,14 +874,9 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     size_t lds_total = lds_bytes;
     // the sphere kernel (one-wave workgroups, compact BVH in L2) while its
     // per-workgroup copy of the pair records is small (rt_kernel.hpp)
-    if (geo == kGeoPairLds && P.nS > 0 && mem == SceneMem::kAuto && lds_bytes <= kSphPairLdsMaxBytes) {
-        if (P.sph_wide && P.sph_wide_stack > 0) {  // the 4-wide BVH: + this wave's walk stacks (u16)
-            geo = kGeoSphWide;
-            lds_total = lds_bytes + (size_t)P.sph_wide_stack * 64u * sizeof(uint16_t);
-        } else if (P.sph_lds) {
-            geo = kGeoSphLds;
-        }
-    }
+    if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto &&
+        lds_bytes <= kSphPairLdsMaxBytes)
+        geo = kGeoSphLds;
     // box clusters whenever rt_create found some; not with
     // spheres, where the sphere walks dominate and the cluster code's register
     // pressure measured 4.6 % slower than the culled pair loop (config 4)
@@ -904,7 +893,7 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
 #ifdef RT_DEV_ISA  // ISA-inspection builds only (tools/isa.sh): the two headline layouts at B = 3
     if (bounces != 3) return hipErrorInvalidValue;
     return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_total, stream)
-                              : launch_g<3, kGeoSphWide>(P, lds_total, stream);
+                              : launch_g<3, kGeoSphLds>(P, lds_total, stream);
 #endif
     switch (bounces) {
         case 0: return launch_b<0>(P, geo, lds_total, stream);

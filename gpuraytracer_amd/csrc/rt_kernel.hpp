@@ -44,9 +44,6 @@ struct KParams {
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
     const uint32_t* sph_lds;  // compact sphere BVH (8 layouts x nE x 16 B), or null
     const uint16_t* sph_lds_id;  // sphere id per compact entry
-    const uint4* sph_wide;    // 4-wide sphere BVH, 4 uint4 per node (rt_scene.cpp build_sphere_wide), or null
-    const uint32_t* sph_wide_id;  // sphere ids of its leaf nodes, 4 per node
-    uint32_t sph_wide_stack;  // walk-stack entries per lane the wide BVH needs (0: not built)
     const float4* tri_nodes;  // triangle BVH (rt_lbvh.hip): 8 layouts x nTN nodes, or null
     const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
     const uint32_t* tri_perm; // BVH leaf order -> triangle id

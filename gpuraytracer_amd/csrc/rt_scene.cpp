@@ -487,138 +487,6 @@ static void build_sphere_lds(CompiledScene* out) {
     out->sph_lds_entries = ne;
 }
 
-// 4-wide BVH over the spheres (rt_trace.hpp sphere_wide_walk): the binary SAH
-// tree collapsed top-down.  A node's children start as the two binary children;
-// while it has fewer than four, the child with the largest box among those
-// holding more than `leaf_max` spheres is replaced by its two children.  A
-// child of at most leaf_max spheres becomes a leaf node (its spheres inline).
-// Boxes are the binary nodes' padded boxes, rounded outward to fp16.  Only
-// speed depends on the tree: every box is a superset of its spheres' boxes.
-constexpr uint32_t kWideStackMax = 40;  // walk-stack entries per lane (u16, LDS)
-struct WideBuild {
-    const BvhBuild& bb;
-    const CompiledScene& cs;
-    uint32_t leaf_max = 4;
-    std::vector<uint32_t> first, count;  // sphere range of every binary node (leaf order)
-    std::vector<uint32_t>* W;
-    std::vector<uint32_t>* I;
-    bool ok = true;
-
-    WideBuild(const BvhBuild& b, const CompiledScene& c) : bb(b), cs(c) {}
-
-    void ranges(uint32_t t) {
-        const BvhBuild::Node& n = bb.tree[t];
-        if (n.count) {
-            first[t] = n.first;
-            count[t] = n.count;
-            return;
-        }
-        ranges(n.left);
-        ranges(n.right);
-        first[t] = first[n.left];
-        count[t] = count[n.left] + count[n.right];
-    }
-    std::vector<uint32_t> children(uint32_t t) const {
-        if (count[t] <= leaf_max) return {t};
-        std::vector<uint32_t> C = {bb.tree[t].left, bb.tree[t].right};
-        while (C.size() < 4) {
-            int pick = -1;
-            double best = -1.0;
-            for (size_t k = 0; k < C.size(); ++k) {
-                const BvhBuild::Node& n = bb.tree[C[k]];
-                if (count[C[k]] <= leaf_max || n.count) continue;
-                const double ar = BvhBuild::area(n.lo, n.hi);
-                if (ar > best) {
-                    best = ar;
-                    pick = (int)k;
-                }
-            }
-            if (pick < 0) break;
-            const uint32_t c = C[pick];
-            C[pick] = bb.tree[c].left;
-            C.insert(C.begin() + pick + 1, bb.tree[c].right);
-        }
-        return C;
-    }
-    // emits the children of inner node `slot` (binary subtree t); returns the
-    // walk-stack bound of the subtree: sum over a root-leaf path of (children - 1)
-    uint32_t emit(uint32_t t, uint32_t slot) {
-        const std::vector<uint32_t> C = children(t);
-        const uint32_t base = (uint32_t)(W->size() / 16);
-        if (base + C.size() > 0x7FFFu) {
-            ok = false;
-            return 0;
-        }
-        W->resize(W->size() + 16 * C.size(), 0u);
-        I->resize(I->size() + 4 * C.size(), 0u);
-        uint16_t lo[3][4], hi[3][4];
-        for (int a = 0; a < 3; ++a)
-            for (int k = 0; k < 4; ++k) {
-                lo[a][k] = 0x7C00u;  // empty slot: +inf .. -inf never hits
-                hi[a][k] = 0xFC00u;
-            }
-        uint32_t leaves = 0, sub = 0;
-        for (size_t k = 0; k < C.size(); ++k) {
-            const BvhBuild::Node& n = bb.tree[C[k]];
-            for (int a = 0; a < 3; ++a) {
-                if (!isfinite(n.lo[a]) || !isfinite(n.hi[a])) ok = false;
-                lo[a][k] = half_dir(n.lo[a], -1);
-                hi[a][k] = half_dir(n.hi[a], +1);
-            }
-            const uint32_t node = base + (uint32_t)k;
-            if (count[C[k]] <= leaf_max) {
-                leaves |= 1u << k;
-                uint32_t* w = W->data() + 16 * (size_t)node;
-                for (uint32_t j = 0; j < 4; ++j) {
-                    float q[4] = {0.0f, 0.0f, 0.0f, -3.0e38f};
-                    uint32_t sid = 0;
-                    if (j < count[C[k]]) {
-                        memcpy(q, cs.sph_isect[first[C[k]] + j].q, sizeof(q));
-                        sid = cs.sph_perm[first[C[k]] + j];
-                    }
-                    memcpy(w + 4 * j, q, sizeof(q));
-                    (*I)[4 * (size_t)node + j] = sid;
-                }
-            } else {
-                sub = std::max(sub, emit(C[k], node));
-            }
-        }
-        uint32_t* w = W->data() + 16 * (size_t)slot;
-        for (int a = 0; a < 3; ++a) {
-            w[4 * a + 0] = lo[a][0] | (uint32_t)lo[a][1] << 16;
-            w[4 * a + 1] = lo[a][2] | (uint32_t)lo[a][3] << 16;
-            w[4 * a + 2] = hi[a][0] | (uint32_t)hi[a][1] << 16;
-            w[4 * a + 3] = hi[a][2] | (uint32_t)hi[a][3] << 16;
-        }
-        w[12] = base;
-        w[13] = leaves;
-        return (uint32_t)C.size() - 1 + sub;
-    }
-};
-
-static void build_sphere_wide(CompiledScene* out, const BvhBuild& bb) {
-    out->sph_wide.clear();
-    out->sph_wide_id.clear();
-    out->sph_wide_stack = 0;
-    if (bb.tree.empty() || bb.leaf_max > 4) return;
-    WideBuild wb(bb, *out);
-    if (const char* lm = getenv("RTPT_WIDE_LEAF")) {  // tuning knob (speed only)
-        const int v = atoi(lm);
-        if (v >= (int)bb.leaf_max && v <= 4) wb.leaf_max = (uint32_t)v;
-    }
-    wb.first.resize(bb.tree.size());
-    wb.count.resize(bb.tree.size());
-    wb.ranges(0);
-    std::vector<uint32_t> W(16, 0u), I(4, 0u);  // node 0: the root
-    wb.W = &W;
-    wb.I = &I;
-    const uint32_t bound = wb.emit(0, 0);
-    if (!wb.ok || bound > kWideStackMax) return;
-    out->sph_wide.swap(W);
-    out->sph_wide_id.swap(I);
-    out->sph_wide_stack = bound + 1;
-}
-
 static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint32_t n,
                              float margin) {
     out->sph_isect.clear();
@@ -654,7 +522,6 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
         memcpy(out->sph_isect[k].q, q, sizeof(q));
     }
     build_sphere_lds(out);
-    build_sphere_wide(out, bb);
 }
 
 // Pair layout: triangles (2k, 2k+1) with the same v0 and one common edge

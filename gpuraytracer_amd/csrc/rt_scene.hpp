@@ -102,18 +102,8 @@ struct CompiledScene {
     // (+,+,+) and (-,-,-), 16 B per entry: inner node = fp16 box (lo rounded
     // down, hi up) + (escape | 0x80000000); leaf (one sphere) = (c.xyz, r*r)
     // fp32, its sphere id in sph_lds_id.  Empty when the tree does not qualify.
-    std::vector<uint32_t> sph_lds;      // 8 layouts x sph_lds_entries x 4 words
-    std::vector<uint16_t> sph_lds_id;   // 8 layouts x sph_lds_entries
-    // 4-wide sphere BVH (rt_trace.hpp sphere_wide_walk): 16
-    // words per node.  Inner node: per axis (lo c0|c1, lo c2|c3, hi c0|c1,
-    // hi c2|c3) as fp16 rounded outward (empty slot: lo +inf, hi -inf), then
-    // (first child, leaf-child mask, 0, 0); the children are consecutive nodes.
-    // Leaf node: up to 4 spheres (c.xyz, r*r) fp32 (empty: r*r = -3e38), their
-    // ids in sph_wide_id[4 * node + j].  Node 0 is the root (inner).  Empty
-    // when the tree does not qualify (> 32767 nodes, stack bound > kWideStackMax).
-    std::vector<uint32_t> sph_wide;
-    std::vector<uint32_t> sph_wide_id;
-    uint32_t sph_wide_stack = 0;        // walk-stack entries a lane can need (bound over root-leaf paths)
+    std::vector<uint32_t> sph_lds;      // 2 layouts x sph_lds_entries x 4 words
+    std::vector<uint16_t> sph_lds_id;   // 2 layouts x sph_lds_entries
     // Box clusters over the pair records: 28 floats each,
     // (u0.xyz, lo0) (u1.xyz, lo1) (u2.xyz, lo2) (hi0, hi1, hi2, flags)
     // (m0, m1, m2, m3) (m4, m5, all, 0) (w0, w1, w2, 0): an oriented box (padded

@@ -139,13 +139,9 @@ enum Geo : int {
     kGeoTriGlobal = 2,  // single-triangle records read from global (big scenes)
     kGeoPairClu = 6,    // pair records in LDS + box clusters
     kGeoSphLds = 7,     // pair records in LDS + the compact sphere BVH in L2 (one-wave workgroups)
-    kGeoSphWide = 8,    // pair records in LDS + the 4-wide sphere BVH in L2, walk stacks in LDS
 };
 
-constexpr bool geo_pairs(int g) {
-    return g == kGeoPairLds || g == kGeoPairSmem || g == kGeoSphLds || g == kGeoSphWide;
-}
-constexpr bool geo_sph_kernel(int g) { return g == kGeoSphLds || g == kGeoSphWide; }
+constexpr bool geo_pairs(int g) { return g == kGeoPairLds || g == kGeoPairSmem || g == kGeoSphLds; }
 
 struct SceneView {
     const float4* tri;        // 3 float4 per triangle (single layout)
@@ -164,9 +160,6 @@ struct SceneView {
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
     const uint4* sent;        // compact sphere BVH entries (kGeoSphLds): 8 octant layouts, global
     const uint16_t* sid;      // sphere id of each compact entry (leaves), global
-    const uint4* swide;       // 4-wide sphere BVH (kGeoSphWide): 64-B nodes, global
-    const uint32_t* swid;     // sphere ids of its leaf nodes, 4 per node
-    __attribute__((address_space(3))) uint16_t* stk;  // this wave's walk stacks in LDS (kGeoSphWide)
     const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
     float* xstash;            // MIS: per-lane primary hit (p, din), SoA in LDS (rt_mis.hip)
 };
@@ -419,151 +412,6 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
                 }
             }
             leaf = kNone;
-        }
-    }
-}
-
-// ---- 4-wide sphere BVH (rt_scene.cpp build_sphere_wide) ----
-// One layout for every ray.  An inner node is 64 B: the fp16 boxes of its up to
-// four children (rounded outward, so still supersets of the padded boxes) as
-// (lo 01, lo 23, hi 01, hi 23) per axis, then the index of its first child (the
-// children are consecutive nodes) and a mask of the children that are leaves.
-// A leaf node holds up to four spheres (c, r*r) in fp32 (empty slots r*r =
-// -3e38: never a positive discriminant); their ids are sph_wide_id[4 * node + j].
-// A step tests ALL children of a node against the ray at once -- a missed child
-// costs nothing more -- so a walk takes a third of the dependent node loads of
-// the binary walk.  Closest-hit walks go to the nearest hit child and push the
-// others far-first on a per-lane stack in LDS (u16 node refs, bit 15 = leaf);
-// any-hit walks take the hits in slot order.  Every sphere a lane can hit lies
-// in a box it enters, so every candidate the brute-force scan would accept is
-// tested, and the (t, id) ranking makes the visiting order free: the result is
-// the oracle's.
-typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
-
-__device__ __forceinline__ float h2f_lo(uint32_t w) { return h2f(w & 0xFFFFu); }
-__device__ __forceinline__ float h2f_hi(uint32_t w) { return h2f(w >> 16); }
-
-template <bool ANY>
-__device__ __forceinline__ void sphere_wide_walk(const uint4* __restrict__ nodes,
-                                                 const uint32_t* __restrict__ ids, uint32_t nT, f3 o, f3 d,
-                                                 float tmin, float& best, int& id, lds_u16_t* stk) {
-    constexpr uint32_t kNone = 0xFFFFFFFFu;
-    const float a = dot(d, d);
-    const RayBox rb = ray_box(o, d);
-    const bool nx = (__float_as_uint(rb.invd.x) >> 31) != 0u;
-    const bool ny = (__float_as_uint(rb.invd.y) >> 31) != 0u;
-    const bool nz = (__float_as_uint(rb.invd.z) >> 31) != 0u;
-    const uint32_t lane = __lane_id();
-    uint32_t cur = (ANY && id >= 0) ? kNone : 0u;  // the root: node 0, inner
-    uint32_t sp = 0;                               // entries on this lane's stack
-    [[maybe_unused]] constexpr int ST = ANY ? 24 : 16;
-    RT_STAT(ST, 1);
-    RT_STAT(ST + 1, __popcll(__ballot(1)));
-    for (;;) {
-        const bool act = cur != kNone;
-        if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-        RT_STAT(ST + 2, 1);
-        RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(act)));
-        if (act) {
-            const uint4* nd = nodes + 4u * (cur & 0x7FFFu);
-            const uint4 e0 = nd[0], e1 = nd[1], e2 = nd[2], e3 = nd[3];
-            uint32_t next = kNone;
-            bool pop = true;
-            if (cur & 0x8000u) {  // leaf: up to four spheres (sph_test, shaders_old.metal:108-136)
-                const uint4 S[4] = {e0, e1, e2, e3};
-                float bq[4], ds[4];
-                uint32_t m = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const f3 oc = o - f3{__uint_as_float(S[j].x), __uint_as_float(S[j].y), __uint_as_float(S[j].z)};
-                    bq[j] = 2.0f * dot(oc, d);
-                    const float cc = dot(oc, oc) - __uint_as_float(S[j].w);
-                    ds[j] = bq[j] * bq[j] - (4.0f * a) * cc;
-                    m |= (ds[j] > 0.0f) ? (1u << j) : 0u;
-                }
-                while (m != 0u) {  // the roots of the spheres with a positive discriminant
-                    const uint32_t j = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1u;
-                    const float b = j == 0 ? bq[0] : j == 1 ? bq[1] : j == 2 ? bq[2] : bq[3];
-                    const float disc = j == 0 ? ds[0] : j == 1 ? ds[1] : j == 2 ? ds[2] : ds[3];
-                    const float sq = sqrtf(disc);
-                    const float a2 = 2.0f * a;
-                    float t = (-b - sq) / a2;
-                    if (!(t > tmin)) t = (-b + sq) / a2;
-                    if (ANY) {
-                        if (t > tmin && t < best) {
-                            id = 0;
-                            m = 0u;
-                            sp = 0u;  // done: nothing more to pop
-                        }
-                    } else if (t > tmin && t < 3.0e38f && t <= best) {
-                        const int s = (int)(nT + ids[4u * (cur & 0x7FFFu) + j]);
-                        if (t < best || s < id) {
-                            best = t;
-                            id = s;
-                        }
-                    }
-                }
-            } else {  // inner: the four child boxes
-                const uint32_t xn0 = nx ? e0.z : e0.x, xn1 = nx ? e0.w : e0.y;
-                const uint32_t xf0 = nx ? e0.x : e0.z, xf1 = nx ? e0.y : e0.w;
-                const uint32_t yn0 = ny ? e1.z : e1.x, yn1 = ny ? e1.w : e1.y;
-                const uint32_t yf0 = ny ? e1.x : e1.z, yf1 = ny ? e1.y : e1.w;
-                const uint32_t zn0 = nz ? e2.z : e2.x, zn1 = nz ? e2.w : e2.y;
-                const uint32_t zf0 = nz ? e2.x : e2.z, zf1 = nz ? e2.y : e2.w;
-                const float tmax = best;
-                uint32_t key[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t xn = k < 2 ? xn0 : xn1, xf = k < 2 ? xf0 : xf1;
-                    const uint32_t yn = k < 2 ? yn0 : yn1, yf = k < 2 ? yf0 : yf1;
-                    const uint32_t zn = k < 2 ? zn0 : zn1, zf = k < 2 ? zf0 : zf1;
-                    const float px = (k & 1) ? h2f_hi(xn) : h2f_lo(xn), qx = (k & 1) ? h2f_hi(xf) : h2f_lo(xf);
-                    const float py = (k & 1) ? h2f_hi(yn) : h2f_lo(yn), qy = (k & 1) ? h2f_hi(yf) : h2f_lo(yf);
-                    const float pz = (k & 1) ? h2f_hi(zn) : h2f_lo(zn), qz = (k & 1) ? h2f_hi(zf) : h2f_lo(zf);
-                    const float tn = vmax3(fmaf(px, rb.invd.x, -rb.oinv.x), fmaf(py, rb.invd.y, -rb.oinv.y),
-                                           vmax(fmaf(pz, rb.invd.z, -rb.oinv.z), tmin));
-                    const float tf = vmin3(fmaf(qx, rb.invd.x, -rb.oinv.x), fmaf(qy, rb.invd.y, -rb.oinv.y),
-                                           vmin(fmaf(qz, rb.invd.z, -rb.oinv.z), tmax));
-                    // closest hit: ordered by the entry distance (its low bits carry the
-                    // slot; speed only); any hit: slot order
-                    key[k] = tn <= tf ? (ANY ? (uint32_t)k : ((__float_as_uint(tn) & ~3u) | (uint32_t)k)) : kNone;
-                }
-                // ascending sort (5 compare-exchanges): hits first -- nearest first
-                // for closest hit, in slot order for any hit
-                auto cas = [](uint32_t& x, uint32_t& y) {
-                    const uint32_t lo = min(x, y), hi = max(x, y);
-                    x = lo;
-                    y = hi;
-                };
-                cas(key[0], key[1]);
-                cas(key[2], key[3]);
-                cas(key[0], key[2]);
-                cas(key[1], key[3]);
-                cas(key[1], key[2]);
-                const uint32_t base = e3.x, leaves = e3.y;
-                auto ref = [&](uint32_t k) {
-                    const uint32_t c = k & 3u;
-                    return (base + c) | (((leaves >> c) & 1u) << 15);
-                };
-                // push the farther hits (far first), go to the nearest
-#pragma unroll
-                for (int k = 3; k >= 1; --k) {
-                    if (key[k] != kNone) {
-                        stk[sp * 64u + lane] = (uint16_t)ref(key[k]);
-                        ++sp;
-                    }
-                }
-                if (key[0] != kNone) {
-                    next = ref(key[0]);
-                    pop = false;
-                }
-            }
-            if (pop && sp > 0u) {
-                --sp;
-                next = stk[sp * 64u + lane];
-            }
-            cur = next;
         }
     }
 }
@@ -947,9 +795,7 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, fl
             }
         }
     }
-    if (SPH && GEO == kGeoSphWide)
-        sphere_wide_walk<false>(sv.swide, sv.swid, sv.nT, o, d, tmin, best, id, sv.stk);
-    else if (SPH && GEO == kGeoSphLds)
+    if (SPH && GEO == kGeoSphLds)
         sphere_walk<false>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
     else if (SPH)
         sphere_closest(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
@@ -1013,12 +859,6 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float
                          &t))
                 return true;
         }
-    }
-    if (SPH && GEO == kGeoSphWide) {
-        float tm = tmax;
-        int id = -1;
-        sphere_wide_walk<true>(sv.swide, sv.swid, sv.nT, o, d, tmin, tm, id, sv.stk);
-        return id >= 0;
     }
     if (SPH && GEO == kGeoSphLds) {
         float tm = tmax;
