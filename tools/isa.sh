@@ -12,6 +12,6 @@ mkdir -p "$(dirname "$OUT")"
 /opt/rocm/bin/hipcc -std=c++17 -O3 -ffp-contract=off -I"$R/include" --offload-arch=gfx950 \
     -fno-slp-vectorize --offload-device-only -S -DRT_DEV_ISA "$@" \
     "$R/gpuraytracer_amd/csrc/rt_kernel.hip" -o "$OUT" 2>/dev/null
-for k in path_trace_kernelILi3ELi6ELb0ELb1ELi4E path_trace_kernelILi3ELi7ELb1ELb1ELi4E; do
+for k in path_trace_kernelILi3ELi6ELb0ELb1ELi4E path_trace_kernelILi3ELi7ELb1ELb1ELi16E; do
     python3 "$R/tools/isa_stats.py" "$OUT" "$k" | head -3
 done
