@@ -149,7 +149,7 @@ struct SceneView {
     const float4* sph;        // 1 float4 per sphere, BVH leaf order
     const float4* node;       // 2 float4 per sphere-BVH node
     const uint32_t* sph_perm; // leaf order -> sphere id (global memory)
-    const float4* tnode;      // triangle BVH: 8 octant layouts of nTN nodes
+    const uint4* tnode;       // triangle BVH: 8 compact octant layouts of nTN nodes
     const float4* tsorted;    // 3 float4 per triangle, BVH leaf order
     const uint32_t* tperm;    // leaf order -> triangle id
     uint32_t nTN;
@@ -416,13 +416,10 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
     }
 }
 
-// Triangle-BVH walks over the compact entries (rt_lbvh.hip: 16 B per node, fp16
-// boxes rounded outward, one layout per direction octant, near child first,
-// stored after the 8 full 32-B layouts): stackless depth-first walks with
+// Triangle-BVH walks over the compact entries (rt_scene.cpp build_tri_sah or
+// rt_lbvh.hip: 16 B per node, fp16 boxes rounded outward, one layout per
+// direction octant, near child first): stackless depth-first walks with
 // conservative boxes and (t, id) ranking.
-__device__ __forceinline__ const uint4* tri_compact(const float4* node, uint32_t nN) {
-    return reinterpret_cast<const uint4*>(node + 16u * nN);
-}
 
 // Wave-packet walks for the coherent camera rays and bounce-0 shadow rays: the
 // wave walks ONE path (the layout of its first lane's octant) and enters a node
@@ -780,10 +777,10 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, fl
     } else if (GEO == kGeoTriBvh) {
         // camera rays: wave packets; bounce rays: per-lane walks with parked leaves
         if (CULL)
-            tri_cbvh_closest_packet(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+            tri_cbvh_closest_packet(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                     best, id);
         else
-            tri_cbvh_walk<false>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+            tri_cbvh_walk<false>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                  best, id);
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
@@ -843,12 +840,12 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float
         }
     } else if (GEO == kGeoTriBvh) {
         if (PACKET) {  // bounce-0 shadow rays: wave packets
-            if (tri_cbvh_any_packet(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o, d, tmin, tmax))
+            if (tri_cbvh_any_packet(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax))
                 return true;
         } else {
             float tm = tmax;
             int hid = -1;
-            tri_cbvh_walk<true>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+            tri_cbvh_walk<true>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                 tm, hid);
             if (hid >= 0) return true;
         }

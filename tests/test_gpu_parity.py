@@ -403,8 +403,13 @@ def ctypes_memmove(dst, src, n):
     ctypes.memmove(ctypes.addressof(dst), ctypes.addressof(src), n)
 
 
+@pytest.mark.parametrize("build", ["sah", "lbvh"])
 @pytest.mark.parametrize("n,dup", [(3000, False), (2500, True)])
-def test_triangle_bvh_gpu_build_bit_exact(n, dup):
+def test_triangle_bvh_gpu_build_bit_exact(n, dup, build, monkeypatch):
+    """Both triangle-BVH builds: the host binned-SAH tree (default) and the
+    GPU Morton LBVH (RTPT_TRI_BUILD=lbvh, rt_lbvh.hip), same compact layout."""
+    if build == "lbvh":
+        monkeypatch.setenv("RTPT_TRI_BUILD", "lbvh")
     s = triangle_soup(40, 24, n, seed=n, dup=dup)
     assert s.describe()["lds_bytes"] == 0  # does not fit LDS: the BVH path
     sd = seed_splitmix(40, 24)
