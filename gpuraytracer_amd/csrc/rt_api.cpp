@@ -669,8 +669,9 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
                     (e = upload(&c->d_tri_perm, perm.data(), perm.size() * sizeof(uint32_t), c->stream)) != hipSuccess) {
                     status = RT_ERR_OUT_OF_MEMORY; msg = std::string("triangle BVH upload: ") + hipGetErrorString(e); break;
                 }
+                c->tri_bvh_nodes = (uint32_t)(nodes.size() / (4 * rt::kTriCompactLayouts));
             }
-            c->tri_bvh_nodes = (uint32_t)nn;
+            if (c->tri_lbvh) c->tri_bvh_nodes = (uint32_t)nn;
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
         if ((e = hipMalloc((void**)&c->d_seeds, npx * sizeof(uint32_t))) != hipSuccess) {

@@ -526,16 +526,22 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
 
 // Triangle BVH built on the host with binned SAH:
 // 32 centroid bins per axis, cost area(left) * n_left + area(right) * n_right,
-// one triangle per leaf, every box padded by the culling margin.  Emitted in
+// leaves of up to kTriLeafMax triangles where the SAH prefers them, every box
+// padded by the culling margin.  Emitted in
 // the compact layout the triangle walks read (rt_trace.hpp tri_cbvh_*): 8
 // depth-first layouts, one per ray-direction octant, near child first along
 // the node's split axis; 16 B per node: the fp16 box rounded outward, then
-// escape | 2^31 (an entry index over all 8 layouts) for an inner node or the
-// triangle's leaf-order index for a leaf.  Only speed depends on the tree.
+// escape | 2^31 (an entry index over all 8 layouts) for an inner node or, for
+// a leaf, its first leaf-order triangle | (count - 1) << 24.  Only speed
+// depends on the tree.
 bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<uint32_t>* nodes,
                    std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm) {
     const uint32_t n = (uint32_t)tri.size();
     if (n == 0 || n >= (1u << 24)) return false;
+    uint32_t leaf_max = kTriLeafMax;  // tuning knobs (speed only)
+    double trav_cost = 1.0;
+    if (const char* v = getenv("RTPT_TRI_LEAF")) leaf_max = (uint32_t)std::min(128, std::max(1, atoi(v)));
+    if (const char* v = getenv("RTPT_TRI_CT")) trav_cost = atof(v);
     std::vector<float> bl(3 * (size_t)n), bh(3 * (size_t)n), cen(3 * (size_t)n);
     for (uint32_t k = 0; k < n; ++k) {
         const float* q = tri[k].q;  // v0 0..2, e1 3..5, e2 6..8 (as refit_kernel sees the triangle)
@@ -591,6 +597,7 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
             continue;
         }
         N.count = 0;
+        const uint32_t nb = J.e - J.b;
         // binned SAH over the centroid bounds of every axis
         double best = INFINITY;
         int best_axis = -1, best_bin = 0;
@@ -642,6 +649,17 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
                     best_axis = a;
                     best_bin = i;
                 }
+            }
+        }
+        // a leaf of up to leaf_max triangles when testing them all costs less
+        // than the split (SAH, a box step costing trav_cost triangle tests)
+        if (nb <= leaf_max) {
+            const float* lo0 = N.lo;  // padded box: only ratios matter
+            const double split = best_axis >= 0 ? trav_cost + best / area(lo0, N.hi) : INFINITY;
+            if ((double)nb <= split) {
+                N.first = J.b;
+                N.count = nb;
+                continue;
             }
         }
         uint32_t mid;
@@ -696,7 +714,7 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
             w[1] = h[2] | (uint32_t)h[3] << 16;
             w[2] = h[4] | (uint32_t)h[5] << 16;
             if (N.count) {
-                w[3] = N.first;  // leaf-order triangle index
+                w[3] = N.first | (N.count - 1u) << 24;  // leaf: first leaf-order triangle, count - 1
             } else {
                 w[3] = (oct * total + idx + size[v]) | 0x80000000u;
                 const bool neg = (oct >> N.axis) & 1u;  // moving toward lower coordinates

@@ -119,8 +119,9 @@ struct CompiledScene {
     std::vector<MisShade> mis_shade;    // by triangle id
 };
 
+constexpr uint32_t kTriLeafMax = 1;  // triangles per leaf of the host SAH build (RTPT_TRI_LEAF)
 // Host binned-SAH triangle BVH in the compact 8-octant layout (rt_scene.cpp):
-// nodes = 8 x (2n - 1) entries of 4 words, sorted = records in leaf order,
+// nodes = 8 layouts x (nodes per layout) entries of 4 words, sorted = records in leaf order,
 // perm = leaf order -> triangle id.  False for n == 0 or n >= 2^24.
 bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<uint32_t>* nodes,
                    std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm);

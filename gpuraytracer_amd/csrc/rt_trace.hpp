@@ -421,6 +421,35 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
 // direction octant, near child first): stackless depth-first walks with
 // conservative boxes and (t, id) ranking.
 
+// A leaf of the triangle BVH: up to 128 consecutive triangles in leaf order,
+// word = first | (count - 1) << 24 (build_tri_sah makes leaves of up to
+// RTPT_TRI_LEAF; the LBVH leaves hold one).  Every triangle is tested with
+// the exact test and ranked by (t, id).
+__device__ __forceinline__ void tri_leaf_closest(const float4* __restrict__ tri, const uint32_t* __restrict__ perm,
+                                                 uint32_t w, f3 o, f3 d, float tmin, float& best, int& id) {
+    const uint32_t first = w & 0xFFFFFFu, cnt = (w >> 24) + 1u;
+    for (uint32_t k = first; k < first + cnt; ++k) {
+        float t;
+        if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f, &t) && t <= best) {
+            const int tid = (int)perm[k];
+            if (t < best || tid < id) {
+                best = t;
+                id = tid;
+            }
+        }
+    }
+}
+__device__ __forceinline__ bool tri_leaf_any(const float4* __restrict__ tri, uint32_t w, f3 o, f3 d, float tmin,
+                                             float tmax) {
+    const uint32_t first = w & 0xFFFFFFu, cnt = (w >> 24) + 1u;
+    bool found = false;
+    for (uint32_t k = first; k < first + cnt && !found; ++k) {
+        float t;
+        found = tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax, &t);
+    }
+    return found;
+}
+
 // Wave-packet walks for the coherent camera rays and bounce-0 shadow rays: the
 // wave walks ONE path (the layout of its first lane's octant) and enters a node
 // when any lane's box test passes; the node index is wave uniform.  A lane whose
@@ -440,16 +469,7 @@ __device__ __forceinline__ void tri_cbvh_closest_packet(const uint4* __restrict_
         if (__builtin_amdgcn_ballot_w64(h) == 0) {
             if (inner) next = e.w & 0x7FFFFFFFu;
         } else if (!inner) {
-            const uint32_t k = e.w;
-            float t;
-            if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f, &t) &&
-                t <= best) {
-                const int tid = (int)perm[k];
-                if (t < best || tid < id) {
-                    best = t;
-                    id = tid;
-                }
-            }
+            tri_leaf_closest(tri, perm, e.w, o, d, tmin, best, id);
         }
         idx = wave_uniform(next);
     }
@@ -470,9 +490,7 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
         if (__builtin_amdgcn_ballot_w64(h) == 0) {
             if (inner) next = e.w & 0x7FFFFFFFu;
         } else if (!inner) {
-            const uint32_t k = e.w;
-            float t;
-            found = found || tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax, &t);
+            found = found || tri_leaf_any(tri, e.w, o, d, tmin, tmax);
             if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
         }
         idx = wave_uniform(next);
@@ -481,7 +499,7 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
 }
 
 // Per-lane compact-BVH walks with POSTPONED LEAVES (as sphere_walk parks its
-// roots): a lane whose box test passes at a leaf parks the triangle and
+// roots): a lane whose box test passes at a leaf parks the leaf and
 // stops; the others walk on until at least 1/kTriParkDen of the lanes
 // still walking are parked, then the wave runs the triangle tests of all
 // parked lanes together -- instead of every mixed step paying for the box
@@ -520,19 +538,13 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
         if (leaf != kNone) {
-            float t;
-            if (tri_test(tri[3 * leaf], tri[3 * leaf + 1], tri[3 * leaf + 2], o, d, tmin,
-                         ANY ? best : 3.0e38f, &t)) {
-                if (ANY) {
+            if (ANY) {
+                if (tri_leaf_any(tri, leaf, o, d, tmin, best)) {
                     id = 0;
                     idx = end;
-                } else if (t <= best) {
-                    const int tid = (int)perm[leaf];
-                    if (t < best || tid < id) {
-                        best = t;
-                        id = tid;
-                    }
                 }
+            } else {
+                tri_leaf_closest(tri, perm, leaf, o, d, tmin, best, id);
             }
             leaf = kNone;
         }
