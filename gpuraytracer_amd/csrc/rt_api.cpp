@@ -36,7 +36,8 @@ struct rt_ctx {
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
     uint32_t* d_sph_perm = nullptr;
-    float4* d_tri_nodes = nullptr;   // GPU-built triangle BVH (rt_lbvh.hip)
+    uint4* d_tri_nodes = nullptr;    // triangle BVH: 8 compact layouts (build_tri_sah / rt_lbvh.hip)
+    bool tri_lbvh = false;           // RTPT_TRI_BUILD=lbvh: GPU Morton LBVH instead of the host SAH build
     float4* d_tri_sorted = nullptr;
     uint32_t* d_tri_perm = nullptr;
     uint32_t tri_bvh_nodes = 0;      // per layout
@@ -594,6 +595,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
     c->device = d->device;
     if (const char* m = getenv("RTPT_LANES")) c->lanes = (uint32_t)atoi(m);
+    if (const char* m = getenv("RTPT_TRI_BUILD")) c->tri_lbvh = !strcmp(m, "lbvh");  // tuning knob
     if (const char* m = getenv("RTPT_SCENE_MEM")) {
         if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
         if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
@@ -645,18 +647,31 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
                                            std::min(lds_pairs, lds_single) > rt::kMaxLdsBytes)));
         if (need_bvh) {
             const size_t nn = 2 * (size_t)nT - 1;
-            // 8 layouts of 32-B nodes, then 8 compact layouts of 16-B entries (rt_lbvh.hip)
-            if ((e = hipMalloc((void**)&c->d_tri_nodes, (8 * nn * 2 + rt::kTriCompactLayouts * nn) * sizeof(float4))) != hipSuccess ||
-                (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
-                (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
-                status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;
+            if (c->tri_lbvh) {  // GPU build (rt_lbvh.hip)
+                if ((e = hipMalloc((void**)&c->d_tri_nodes, rt::kTriCompactLayouts * nn * sizeof(uint4))) != hipSuccess ||
+                    (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
+                    (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
+                    status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;
+                }
+                if ((e = rt::build_tri_lbvh(c->d_tri_isect, nT, s.tri_lo, s.tri_hi, s.margin, c->d_tri_nodes,
+                                            c->d_tri_sorted, c->d_tri_perm, c->stream)) != hipSuccess) {
+                    status = (e == hipErrorInvalidValue) ? RT_ERR_INVALID_ARG : RT_ERR_LAUNCH;
+                    msg = std::string("triangle BVH build: ") + hipGetErrorString(e); break;
+                }
+            } else {  // host binned SAH (rt_scene.cpp build_tri_sah), uploaded
+                std::vector<uint32_t> nodes, perm;
+                std::vector<rt::TriIsect> sorted;
+                if (!rt::build_tri_sah(s.tri_isect, s.margin, &nodes, &sorted, &perm)) {
+                    status = RT_ERR_INVALID_ARG; msg = "triangle BVH build: too many triangles (2^24)"; break;
+                }
+                if ((e = upload(&c->d_tri_nodes, nodes.data(), nodes.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
+                    (e = upload(&c->d_tri_sorted, sorted.data(), sorted.size() * sizeof(rt::TriIsect), c->stream)) != hipSuccess ||
+                    (e = upload(&c->d_tri_perm, perm.data(), perm.size() * sizeof(uint32_t), c->stream)) != hipSuccess) {
+                    status = RT_ERR_OUT_OF_MEMORY; msg = std::string("triangle BVH upload: ") + hipGetErrorString(e); break;
+                }
+                c->tri_bvh_nodes = (uint32_t)(nodes.size() / (4 * rt::kTriCompactLayouts));
             }
-            if ((e = rt::build_tri_lbvh(c->d_tri_isect, nT, s.tri_lo, s.tri_hi, s.margin, c->d_tri_nodes,
-                                        c->d_tri_sorted, c->d_tri_perm, c->stream)) != hipSuccess) {
-                status = (e == hipErrorInvalidValue) ? RT_ERR_INVALID_ARG : RT_ERR_LAUNCH;
-                msg = std::string("triangle BVH build: ") + hipGetErrorString(e); break;
-            }
-            c->tri_bvh_nodes = (uint32_t)nn;
+            if (c->tri_lbvh) c->tri_bvh_nodes = (uint32_t)nn;
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
         if ((e = hipMalloc((void**)&c->d_seeds, npx * sizeof(uint32_t))) != hipSuccess) {

@@ -26,8 +26,8 @@ constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padde
 constexpr uint32_t kSphBlockThreads = 64;
 constexpr size_t kSphPairLdsMaxBytes = 4 * 1024;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
-// Compact layouts of the triangle BVH (rt_lbvh.hip, rt_trace.hpp tri_cbvh_*):
-// one per direction octant, 16 B per node, stored after the 8 full 32-B layouts.
+// Layouts of the triangle BVH (rt_scene.cpp build_tri_sah / rt_lbvh.hip,
+// rt_trace.hpp tri_cbvh_*): one per direction octant, 16 B per node.
 constexpr uint32_t kTriCompactLayouts = 8;
 // Above this many triangles rt_create builds the triangle BVH (measured crossover
 // of the LDS brute-force layouts and the BVH walks on random triangles: ~300).
@@ -44,7 +44,7 @@ struct KParams {
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
     const uint32_t* sph_lds;  // compact sphere BVH (8 layouts x nE x 16 B), or null
     const uint16_t* sph_lds_id;  // sphere id per compact entry
-    const float4* tri_nodes;  // triangle BVH (rt_lbvh.hip): 8 layouts x nTN nodes, or null
+    const uint4* tri_nodes;   // triangle BVH: 8 compact layouts x nTN nodes, or null
     const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
     const uint32_t* tri_perm; // BVH leaf order -> triangle id
     const uint32_t* seeds;    // W*H, full frame
@@ -85,7 +85,7 @@ hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds
 // shaders.metal:635-707).
 struct MisParams {
     const float4* tri_isect;   // 3 float4 per triangle
-    const float4* tri_nodes;   // triangle BVH or null (as KParams)
+    const uint4* tri_nodes;    // triangle BVH or null (as KParams)
     const float4* tri_sorted;
     const uint32_t* tri_perm;
     uint32_t nTN;
@@ -108,10 +108,10 @@ struct MisParams {
 hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream);
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs);
 
-// GPU build of the triangle BVH (rt_lbvh.hip).  d_nodes: 8 * (2n-1) * 2 float4,
+// GPU build of the triangle BVH (rt_lbvh.hip).  d_nodes: 8 * (2n-1) uint4,
 // d_sorted: 3n float4, d_perm: n.  Synchronises the stream.
 hipError_t build_tri_lbvh(const float4* d_tri, uint32_t n, const float lo[3], const float hi[3],
-                          float margin, float4* d_nodes, float4* d_sorted, uint32_t* d_perm,
+                          float margin, uint4* d_nodes, float4* d_sorted, uint32_t* d_perm,
                           hipStream_t s);
 
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);

@@ -6,10 +6,12 @@
 // device radix sort (hipCUB, stable: equal codes stay in id order, so the build
 // is deterministic), one thread per inner node finds its key range and split,
 // leaves are refitted bottom-up with acquire/release counters, and the tree is
-// written in the same stackless layout as the host-built sphere BVH
-// (rt_scene.hpp BvhNode): 8 depth-first layouts, one per ray-direction octant,
-// near child first along the node's split axis, every box padded by the
-// culling margin.  One triangle per leaf.  Only speed depends on the tree: the
+// written in the compact stackless layout the triangle walks read (16-B
+// entries, rt_trace.hpp tri_cbvh_*): 8 depth-first layouts, one per
+// ray-direction octant, near child first along the node's split axis, every
+// box padded by the culling margin.  One triangle per leaf.  The default
+// build is the host binned-SAH one (rt_scene.cpp build_tri_sah, same layout);
+// this GPU build is taken with RTPT_TRI_BUILD=lbvh.  Only speed depends on the tree: the
 // walks in rt_trace.hpp return the brute-force (t, id) minimum.
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
@@ -138,7 +140,7 @@ __device__ __forceinline__ uint32_t subtree_nodes(const uint32_t* range, uint32_
 __global__ void layout_kernel(uint32_t n, const uint32_t* __restrict__ child,
                               const uint32_t* __restrict__ parent,
                               const uint32_t* __restrict__ range, const uint8_t* __restrict__ axis,
-                              const float4* __restrict__ box, float4* __restrict__ nodes) {
+                              const float4* __restrict__ box, uint4* __restrict__ nodes) {
     const uint32_t total = 2 * n - 1;
     const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t oct = blockIdx.y;
@@ -152,25 +154,17 @@ __global__ void layout_kernel(uint32_t n, const uint32_t* __restrict__ child,
         c = p;
     }
     const uint32_t escape = idx + subtree_nodes(range, n, v);
-    const uint32_t leaf = (v >= n - 1) ? ((1u << 24) | (v - (n - 1))) : 0u;
     const float4 b0 = box[2 * v], b1 = box[2 * v + 1];
-    float4* o = nodes + 2 * ((size_t)oct * total + idx);
-    o[0] = make_float4(b0.x, b0.y, b0.z, __uint_as_float(escape));
-    o[1] = make_float4(b1.x, b1.y, b1.z, __uint_as_float(leaf));
-    {
-        // compact 16-B entries (every octant's layout), after the 8 full layouts
-        // (rt_trace.hpp tri_cbvh_*): the box in fp16 rounded outward (a
-        // superset of the padded box), then escape | 2^31 for an inner node (an
-        // entry index over all compact layouts) or the leaf's triangle index in
-        // leaf order (a leaf's escape is the next entry)
-        const uint32_t lay = oct;
-        uint4* cn = reinterpret_cast<uint4*>(nodes + 2 * (size_t)8 * total) + (size_t)lay * total + idx;
-        const uint32_t h0 = __half_as_ushort(__float2half_rd(b0.x)), h1 = __half_as_ushort(__float2half_rd(b0.y));
-        const uint32_t h2 = __half_as_ushort(__float2half_rd(b0.z)), h3 = __half_as_ushort(__float2half_ru(b1.x));
-        const uint32_t h4 = __half_as_ushort(__float2half_ru(b1.y)), h5 = __half_as_ushort(__float2half_ru(b1.z));
-        const uint32_t w = (v >= n - 1) ? (v - (n - 1)) : ((lay * total + escape) | 0x80000000u);
-        *cn = make_uint4(h0 | (h1 << 16), h2 | (h3 << 16), h4 | (h5 << 16), w);
-    }
+    // compact 16-B entries (rt_trace.hpp tri_cbvh_*): the box in fp16 rounded
+    // outward (a superset of the padded box), then escape | 2^31 for an inner
+    // node (an entry index over all 8 layouts) or the leaf's triangle index in
+    // leaf order (a leaf's escape is the next entry)
+    uint4* cn = nodes + (size_t)oct * total + idx;
+    const uint32_t h0 = __half_as_ushort(__float2half_rd(b0.x)), h1 = __half_as_ushort(__float2half_rd(b0.y));
+    const uint32_t h2 = __half_as_ushort(__float2half_rd(b0.z)), h3 = __half_as_ushort(__float2half_ru(b1.x));
+    const uint32_t h4 = __half_as_ushort(__float2half_ru(b1.y)), h5 = __half_as_ushort(__float2half_ru(b1.z));
+    const uint32_t w = (v >= n - 1) ? (v - (n - 1)) : ((oct * total + escape) | 0x80000000u);
+    *cn = make_uint4(h0 | (h1 << 16), h2 | (h3 << 16), h4 | (h5 << 16), w);
 }
 
 __global__ void gather_kernel(const float4* __restrict__ tri, const uint32_t* __restrict__ ids,
@@ -191,7 +185,7 @@ hipError_t dalloc(T** p, size_t count) {
 }  // namespace
 
 hipError_t build_tri_lbvh(const float4* d_tri, uint32_t n, const float lo[3], const float hi[3],
-                          float margin, float4* d_nodes, float4* d_sorted, uint32_t* d_perm,
+                          float margin, uint4* d_nodes, float4* d_sorted, uint32_t* d_perm,
                           hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (n >= (1u << 24)) return hipErrorInvalidValue;  // leaf index field is 24 bits

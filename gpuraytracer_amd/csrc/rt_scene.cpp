@@ -524,6 +524,215 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
     build_sphere_lds(out);
 }
 
+// Triangle BVH built on the host with binned SAH:
+// 32 centroid bins per axis, cost area(left) * n_left + area(right) * n_right,
+// leaves of up to kTriLeafMax triangles where the SAH prefers them, every box
+// padded by the culling margin.  Emitted in
+// the compact layout the triangle walks read (rt_trace.hpp tri_cbvh_*): 8
+// depth-first layouts, one per ray-direction octant, near child first along
+// the node's split axis; 16 B per node: the fp16 box rounded outward, then
+// escape | 2^31 (an entry index over all 8 layouts) for an inner node or, for
+// a leaf, its first leaf-order triangle | (count - 1) << 24.  Only speed
+// depends on the tree.
+bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<uint32_t>* nodes,
+                   std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm) {
+    const uint32_t n = (uint32_t)tri.size();
+    if (n == 0 || n >= (1u << 24)) return false;
+    uint32_t leaf_max = kTriLeafMax;  // tuning knobs (speed only)
+    double trav_cost = 1.0;
+    if (const char* v = getenv("RTPT_TRI_LEAF")) leaf_max = (uint32_t)std::min(128, std::max(1, atoi(v)));
+    if (const char* v = getenv("RTPT_TRI_CT")) trav_cost = atof(v);
+    std::vector<float> bl(3 * (size_t)n), bh(3 * (size_t)n), cen(3 * (size_t)n);
+    for (uint32_t k = 0; k < n; ++k) {
+        const float* q = tri[k].q;  // v0 0..2, e1 3..5, e2 6..8 (as refit_kernel sees the triangle)
+        for (int a = 0; a < 3; ++a) {
+            const float v0 = q[a], v1 = q[a] + q[3 + a], v2 = q[a] + q[6 + a];
+            bl[3 * k + a] = fminf(v0, fminf(v1, v2));
+            bh[3 * k + a] = fmaxf(v0, fmaxf(v1, v2));
+            cen[3 * k + a] = 0.5f * (bl[3 * k + a] + bh[3 * k + a]);
+        }
+    }
+    struct Node {
+        float lo[3], hi[3];
+        int axis;
+        uint32_t left, right, first, count;
+    };
+    std::vector<Node> tree;
+    tree.reserve(2 * (size_t)n);
+    std::vector<uint32_t> ids(n);
+    for (uint32_t k = 0; k < n; ++k) ids[k] = k;
+    constexpr int kBins = 32;
+    auto area = [](const float* lo, const float* hi) {
+        const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+        return x * y + y * z + z * x;
+    };
+    // iterative build (deep trees must not exhaust the host stack)
+    struct Job { uint32_t node, b, e; };
+    std::vector<Job> jobs;
+    tree.push_back(Node{});
+    jobs.push_back({0, 0, n});
+    while (!jobs.empty()) {
+        const Job J = jobs.back();
+        jobs.pop_back();
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t k = J.b; k < J.e; ++k) {
+            const uint32_t t = ids[k];
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = fminf(lo[a], bl[3 * t + a]);
+                hi[a] = fmaxf(hi[a], bh[3 * t + a]);
+                clo[a] = fminf(clo[a], cen[3 * t + a]);
+                chi[a] = fmaxf(chi[a], cen[3 * t + a]);
+            }
+        }
+        Node& N = tree[J.node];
+        for (int a = 0; a < 3; ++a) {
+            N.lo[a] = lo[a] - margin;
+            N.hi[a] = hi[a] + margin;
+        }
+        N.axis = 0;
+        if (J.e - J.b == 1) {
+            N.first = J.b;
+            N.count = 1;
+            continue;
+        }
+        N.count = 0;
+        const uint32_t nb = J.e - J.b;
+        // binned SAH over the centroid bounds of every axis
+        double best = INFINITY;
+        int best_axis = -1, best_bin = 0;
+        for (int a = 0; a < 3; ++a) {
+            const float ext = chi[a] - clo[a];
+            if (!(ext > 0.0f)) continue;
+            const float scale = (float)kBins / ext;
+            float blo[kBins][3], bhi[kBins][3];
+            uint32_t cnt[kBins] = {0};
+            for (int i = 0; i < kBins; ++i)
+                for (int q = 0; q < 3; ++q) {
+                    blo[i][q] = INFINITY;
+                    bhi[i][q] = -INFINITY;
+                }
+            for (uint32_t k = J.b; k < J.e; ++k) {
+                const uint32_t t = ids[k];
+                const int bi = std::min(kBins - 1, (int)((cen[3 * t + a] - clo[a]) * scale));
+                ++cnt[bi];
+                for (int q = 0; q < 3; ++q) {
+                    blo[bi][q] = fminf(blo[bi][q], bl[3 * t + q]);
+                    bhi[bi][q] = fmaxf(bhi[bi][q], bh[3 * t + q]);
+                }
+            }
+            double right_area[kBins];
+            uint32_t right_cnt[kBins];
+            float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t rc = 0;
+            for (int i = kBins - 1; i >= 1; --i) {  // right part = bins [i, kBins)
+                rc += cnt[i];
+                for (int q = 0; q < 3; ++q) {
+                    rlo[q] = fminf(rlo[q], blo[i][q]);
+                    rhi[q] = fmaxf(rhi[q], bhi[i][q]);
+                }
+                right_area[i] = rc ? area(rlo, rhi) : 0.0;
+                right_cnt[i] = rc;
+            }
+            float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t lc = 0;
+            for (int i = 1; i < kBins; ++i) {  // left part = bins [0, i)
+                lc += cnt[i - 1];
+                for (int q = 0; q < 3; ++q) {
+                    llo[q] = fminf(llo[q], blo[i - 1][q]);
+                    lhi[q] = fmaxf(lhi[q], bhi[i - 1][q]);
+                }
+                if (lc == 0 || right_cnt[i] == 0) continue;
+                const double c = area(llo, lhi) * lc + right_area[i] * right_cnt[i];
+                if (c < best) {
+                    best = c;
+                    best_axis = a;
+                    best_bin = i;
+                }
+            }
+        }
+        // a leaf of up to leaf_max triangles when testing them all costs less
+        // than the split (SAH, a box step costing trav_cost triangle tests)
+        if (nb <= leaf_max) {
+            const float* lo0 = N.lo;  // padded box: only ratios matter
+            const double split = best_axis >= 0 ? trav_cost + best / area(lo0, N.hi) : INFINITY;
+            if ((double)nb <= split) {
+                N.first = J.b;
+                N.count = nb;
+                continue;
+            }
+        }
+        uint32_t mid;
+        if (best_axis >= 0) {
+            const int a = best_axis;
+            const float scale = (float)kBins / (chi[a] - clo[a]);
+            const float c0 = clo[a];
+            auto it = std::partition(ids.begin() + J.b, ids.begin() + J.e, [&](uint32_t t) {
+                return std::min(kBins - 1, (int)((cen[3 * t + a] - c0) * scale)) < best_bin;
+            });
+            mid = (uint32_t)(it - ids.begin());
+            N.axis = a;
+        } else {  // every centroid in one point: split by index
+            mid = J.b + (J.e - J.b) / 2;
+            int a = 0;
+            for (int q = 1; q < 3; ++q)
+                if (hi[q] - lo[q] > hi[a] - lo[a]) a = q;
+            N.axis = a;
+        }
+        if (mid == J.b || mid == J.e) mid = J.b + (J.e - J.b) / 2;
+        const uint32_t l = (uint32_t)tree.size();
+        tree.push_back(Node{});
+        const uint32_t r = (uint32_t)tree.size();
+        tree.push_back(Node{});
+        tree[J.node].left = l;
+        tree[J.node].right = r;
+        jobs.push_back({r, mid, J.e});
+        jobs.push_back({l, J.b, mid});
+    }
+    const uint32_t total = (uint32_t)tree.size();  // 2n - 1
+    // subtree entry counts (one entry per node)
+    std::vector<uint32_t> size(total, 1u);
+    for (uint32_t i = total; i-- > 0;)  // children are created after their parent
+        if (!tree[i].count) size[i] = 1u + size[tree[i].left] + size[tree[i].right];
+    nodes->assign((size_t)8 * total * 4, 0u);
+    for (uint32_t oct = 0; oct < 8; ++oct) {
+        uint32_t* L = nodes->data() + (size_t)oct * total * 4;
+        // explicit-stack preorder: (node, entry index)
+        std::vector<std::pair<uint32_t, uint32_t>> st;
+        st.push_back({0u, 0u});
+        while (!st.empty()) {
+            const auto [v, idx] = st.back();
+            st.pop_back();
+            const Node& N = tree[v];
+            uint16_t h[6];
+            for (int a = 0; a < 3; ++a) {
+                h[a] = half_dir(N.lo[a], -1);
+                h[3 + a] = half_dir(N.hi[a], +1);
+            }
+            uint32_t* w = L + 4 * (size_t)idx;
+            w[0] = h[0] | (uint32_t)h[1] << 16;
+            w[1] = h[2] | (uint32_t)h[3] << 16;
+            w[2] = h[4] | (uint32_t)h[5] << 16;
+            if (N.count) {
+                w[3] = N.first | (N.count - 1u) << 24;  // leaf: first leaf-order triangle, count - 1
+            } else {
+                w[3] = (oct * total + idx + size[v]) | 0x80000000u;
+                const bool neg = (oct >> N.axis) & 1u;  // moving toward lower coordinates
+                const uint32_t near = neg ? N.right : N.left, far = neg ? N.left : N.right;
+                st.push_back({far, idx + 1 + size[near]});
+                st.push_back({near, idx + 1});
+            }
+        }
+    }
+    sorted->resize(n);
+    perm->resize(n);
+    for (uint32_t k = 0; k < n; ++k) {
+        (*sorted)[k] = tri[ids[k]];
+        (*perm)[k] = ids[k];
+    }
+    return true;
+}
+
 // Pair layout: triangles (2k, 2k+1) with the same v0 and one common edge
 // vector S (bitwise, as computed above).  All-or-nothing, so the kernel keeps
 // testing primitives in id order.

@@ -119,6 +119,13 @@ struct CompiledScene {
     std::vector<MisShade> mis_shade;    // by triangle id
 };
 
+constexpr uint32_t kTriLeafMax = 1;  // triangles per leaf of the host SAH build (RTPT_TRI_LEAF)
+// Host binned-SAH triangle BVH in the compact 8-octant layout (rt_scene.cpp):
+// nodes = 8 layouts x (nodes per layout) entries of 4 words, sorted = records in leaf order,
+// perm = leaf order -> triangle id.  False for n == 0 or n >= 2^24.
+bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<uint32_t>* nodes,
+                   std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm);
+
 // Validates and precomputes; returns false with *err set on bad input.
 bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float3* verts,
                    uint32_t n_tri, const SquareLightGPU& light, const SphereGPU* spheres,

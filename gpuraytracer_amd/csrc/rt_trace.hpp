@@ -149,7 +149,7 @@ struct SceneView {
     const float4* sph;        // 1 float4 per sphere, BVH leaf order
     const float4* node;       // 2 float4 per sphere-BVH node
     const uint32_t* sph_perm; // leaf order -> sphere id (global memory)
-    const float4* tnode;      // triangle BVH: 8 octant layouts of nTN nodes
+    const uint4* tnode;       // triangle BVH: 8 compact octant layouts of nTN nodes
     const float4* tsorted;    // 3 float4 per triangle, BVH leaf order
     const uint32_t* tperm;    // leaf order -> triangle id
     uint32_t nTN;
@@ -416,12 +416,38 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
     }
 }
 
-// Triangle-BVH walks over the compact entries (rt_lbvh.hip: 16 B per node, fp16
-// boxes rounded outward, one layout per direction octant, near child first,
-// stored after the 8 full 32-B layouts): stackless depth-first walks with
+// Triangle-BVH walks over the compact entries (rt_scene.cpp build_tri_sah or
+// rt_lbvh.hip: 16 B per node, fp16 boxes rounded outward, one layout per
+// direction octant, near child first): stackless depth-first walks with
 // conservative boxes and (t, id) ranking.
-__device__ __forceinline__ const uint4* tri_compact(const float4* node, uint32_t nN) {
-    return reinterpret_cast<const uint4*>(node + 16u * nN);
+
+// A leaf of the triangle BVH: up to 128 consecutive triangles in leaf order,
+// word = first | (count - 1) << 24 (build_tri_sah makes leaves of up to
+// RTPT_TRI_LEAF; the LBVH leaves hold one).  Every triangle is tested with
+// the exact test and ranked by (t, id).
+__device__ __forceinline__ void tri_leaf_closest(const float4* __restrict__ tri, const uint32_t* __restrict__ perm,
+                                                 uint32_t w, f3 o, f3 d, float tmin, float& best, int& id) {
+    const uint32_t first = w & 0xFFFFFFu, cnt = (w >> 24) + 1u;
+    for (uint32_t k = first; k < first + cnt; ++k) {
+        float t;
+        if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f, &t) && t <= best) {
+            const int tid = (int)perm[k];
+            if (t < best || tid < id) {
+                best = t;
+                id = tid;
+            }
+        }
+    }
+}
+__device__ __forceinline__ bool tri_leaf_any(const float4* __restrict__ tri, uint32_t w, f3 o, f3 d, float tmin,
+                                             float tmax) {
+    const uint32_t first = w & 0xFFFFFFu, cnt = (w >> 24) + 1u;
+    bool found = false;
+    for (uint32_t k = first; k < first + cnt && !found; ++k) {
+        float t;
+        found = tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax, &t);
+    }
+    return found;
 }
 
 // Wave-packet walks for the coherent camera rays and bounce-0 shadow rays: the
@@ -443,16 +469,7 @@ __device__ __forceinline__ void tri_cbvh_closest_packet(const uint4* __restrict_
         if (__builtin_amdgcn_ballot_w64(h) == 0) {
             if (inner) next = e.w & 0x7FFFFFFFu;
         } else if (!inner) {
-            const uint32_t k = e.w;
-            float t;
-            if (tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, 3.0e38f, &t) &&
-                t <= best) {
-                const int tid = (int)perm[k];
-                if (t < best || tid < id) {
-                    best = t;
-                    id = tid;
-                }
-            }
+            tri_leaf_closest(tri, perm, e.w, o, d, tmin, best, id);
         }
         idx = wave_uniform(next);
     }
@@ -473,9 +490,7 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
         if (__builtin_amdgcn_ballot_w64(h) == 0) {
             if (inner) next = e.w & 0x7FFFFFFFu;
         } else if (!inner) {
-            const uint32_t k = e.w;
-            float t;
-            found = found || tri_test(tri[3 * k], tri[3 * k + 1], tri[3 * k + 2], o, d, tmin, tmax, &t);
+            found = found || tri_leaf_any(tri, e.w, o, d, tmin, tmax);
             if (__builtin_amdgcn_ballot_w64(!found) == 0) break;
         }
         idx = wave_uniform(next);
@@ -484,7 +499,7 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
 }
 
 // Per-lane compact-BVH walks with POSTPONED LEAVES (as sphere_walk parks its
-// roots): a lane whose box test passes at a leaf parks the triangle and
+// roots): a lane whose box test passes at a leaf parks the leaf and
 // stops; the others walk on until at least 1/kTriParkDen of the lanes
 // still walking are parked, then the wave runs the triangle tests of all
 // parked lanes together -- instead of every mixed step paying for the box
@@ -523,19 +538,13 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
         if (leaf != kNone) {
-            float t;
-            if (tri_test(tri[3 * leaf], tri[3 * leaf + 1], tri[3 * leaf + 2], o, d, tmin,
-                         ANY ? best : 3.0e38f, &t)) {
-                if (ANY) {
+            if (ANY) {
+                if (tri_leaf_any(tri, leaf, o, d, tmin, best)) {
                     id = 0;
                     idx = end;
-                } else if (t <= best) {
-                    const int tid = (int)perm[leaf];
-                    if (t < best || tid < id) {
-                        best = t;
-                        id = tid;
-                    }
                 }
+            } else {
+                tri_leaf_closest(tri, perm, leaf, o, d, tmin, best, id);
             }
             leaf = kNone;
         }
@@ -780,10 +789,10 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, fl
     } else if (GEO == kGeoTriBvh) {
         // camera rays: wave packets; bounce rays: per-lane walks with parked leaves
         if (CULL)
-            tri_cbvh_closest_packet(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+            tri_cbvh_closest_packet(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                     best, id);
         else
-            tri_cbvh_walk<false>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+            tri_cbvh_walk<false>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                  best, id);
     } else {
         for (uint32_t k = 0; k < sv.nT; ++k) {
@@ -843,12 +852,12 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float
         }
     } else if (GEO == kGeoTriBvh) {
         if (PACKET) {  // bounce-0 shadow rays: wave packets
-            if (tri_cbvh_any_packet(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.nTN, o, d, tmin, tmax))
+            if (tri_cbvh_any_packet(sv.tnode, sv.tsorted, sv.nTN, o, d, tmin, tmax))
                 return true;
         } else {
             float tm = tmax;
             int hid = -1;
-            tri_cbvh_walk<true>(tri_compact(sv.tnode, sv.nTN), sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
+            tri_cbvh_walk<true>(sv.tnode, sv.tsorted, sv.tperm, sv.nTN, o, d, tmin,
                                 tm, hid);
             if (hid >= 0) return true;
         }

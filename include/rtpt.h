@@ -275,7 +275,7 @@ typedef struct rt_scene_info {
     uint32_t n_spheres;
     uint32_t lds_bytes;          /* intersection records staged per workgroup (0: read from global) */
     uint32_t n_sphere_nodes;     /* sphere BVH nodes per layout (32 B each, 8 layouts, global) */
-    uint32_t n_triangle_bvh_nodes; /* GPU-built triangle BVH nodes per layout (0: LDS layouts) */
+    uint32_t n_triangle_bvh_nodes; /* triangle BVH nodes per layout, 2n - 1 at one triangle per leaf (0: LDS layouts) */
     uint32_t n_box_clusters;     /* pair runs on the faces of one oriented box (slab-tested first) */
     uint32_t pair_free_mask;     /* pairs in no box cluster (bit k = pair k) */
     uint32_t sphere_kernel_lds_bytes; /* dynamic LDS of the sphere kernel (its pair records; 0: sphere kernel not taken) */

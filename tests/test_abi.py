@@ -104,6 +104,48 @@ def test_scene_layout_uses_shared_edge_pairs():
     assert big["n_sphere_nodes"] == bvh_nodes(5000)
 
 
+def _with_quads(base, n_quads, seed=3):
+    """base's triangles + n_quads random planar quads (one shared-edge pair each)."""
+    import ctypes
+    rng = np.random.default_rng(seed)
+    n0 = base.n_triangles
+    n = n0 + 2 * n_quads
+    mats = (g.MaterialGPU * n)()
+    verts = (g.float3 * (3 * n))()
+    ctypes.memmove(ctypes.addressof(mats), ctypes.addressof(base.materials), n0 * 48)
+    ctypes.memmove(ctypes.addressof(verts), ctypes.addressof(base.vertices), 3 * n0 * 16)
+    vv = np.frombuffer(verts, np.float32).reshape(-1, 4)
+    mm = np.frombuffer(mats, np.float32).reshape(-1, 12)
+    for q in range(n_quads):
+        c = rng.uniform(-2.0, 2.0, 3)
+        a, b = rng.normal(size=3) * 0.3, rng.normal(size=3) * 0.3
+        P = [c, c + a, c + a + b, c + b]
+        for t, tri in enumerate(((P[0], P[1], P[2]), (P[0], P[2], P[3]))):
+            k = n0 + 2 * q + t
+            vv[3 * k:3 * k + 3, :3] = np.array(tri, np.float32)
+            mm[k, 0:3] = 0.5
+            mm[k, 3] = 1.0
+    return mats, verts
+
+
+def test_sphere_kernel_pair_budget():
+    """The one-wave sphere kernel stages the pair records in every workgroup, so
+    it is taken only while they fit kSphPairLdsMaxBytes (4 KB, rt_kernel.hpp);
+    above it the pair kernel (records shared by 256 threads) serves the scene."""
+    base = g.Scene.cornell_box(64, 48)
+    sph = g.Scene.random_spheres(64, 48, 200).spheres
+    mixed = g.Scene(base.camera, base.materials, base.vertices, base.light, sph)
+    info = mixed.describe()
+    assert info["n_triangle_pairs"] == 18 and info["sphere_kernel_lds_bytes"] == 18 * 112
+    mats, verts = _with_quads(base, 18)  # 36 pairs = 4032 B: still the sphere kernel
+    at = g.Scene(base.camera, mats, verts, base.light, sph).describe()
+    assert at["n_triangle_pairs"] == 36 and at["sphere_kernel_lds_bytes"] == 36 * 112
+    mats, verts = _with_quads(base, 19)  # 37 pairs = 4144 B > 4 KB
+    over = g.Scene(base.camera, mats, verts, base.light, sph).describe()
+    assert over["n_triangle_pairs"] == 37 and over["sphere_kernel_lds_bytes"] == 0
+    assert over["lds_bytes"] == 37 * 112
+
+
 def test_portrait_resolution_is_rejected():
     """The reference computes aspect = float(res.x / res.y) in integers
     (sampling.metal:132): a portrait frame gives aspect 0 and halfHeight inf.

@@ -259,6 +259,27 @@ def test_spheres_16_lanes_frame_and_rows_bit_exact_vs_oracle():
     assert_parity(tile, ref[3::8], "spheres rows 3::8, 16 lanes")
 
 
+def test_mixed_scene_sphere_kernel_and_pair_fallback_bit_exact():
+    """Cornell box (36 triangles, both boxes) + 300 spheres: the one-wave sphere
+    kernel; with 19 more quads (37 pairs, over the 4 KB per-workgroup budget) the
+    pair kernel with the 32-B-node sphere walks.  Both are the oracle."""
+    from test_abi import _with_quads
+    base = Scene.cornell_box(48, 32)
+    sph = Scene.random_spheres(48, 32, 300, seed=21).spheres
+    sd = seed_splitmix(48, 32, key=21)
+    for n_quads, sphere_kernel in ((0, True), (19, False)):
+        if n_quads:
+            mats, verts = _with_quads(base, n_quads)
+            s = Scene(base.camera, mats, verts, base.light, sph)
+        else:
+            s = Scene(base.camera, base.materials, base.vertices, base.light, sph)
+        with Renderer(s, seeds=sd) as r:
+            out = r.render(RenderParams(spp=3, bounces=3))
+            k = r.last_launch()["kernel"]
+        assert (k.startswith("rt::path_trace_kernel<3, 7,") or k.startswith("rt::path_trace_kernel<3, 8,")) == sphere_kernel, k
+        assert_parity(out, oracle_lib.render(s, sd, 3, 3), f"mixed +{n_quads} quads")
+
+
 def test_errors_are_status_codes():
     s = Scene.cornell_box(16, 8)
     with Renderer(s) as r:
@@ -403,8 +424,13 @@ def ctypes_memmove(dst, src, n):
     ctypes.memmove(ctypes.addressof(dst), ctypes.addressof(src), n)
 
 
+@pytest.mark.parametrize("build", ["sah", "lbvh"])
 @pytest.mark.parametrize("n,dup", [(3000, False), (2500, True)])
-def test_triangle_bvh_gpu_build_bit_exact(n, dup):
+def test_triangle_bvh_gpu_build_bit_exact(n, dup, build, monkeypatch):
+    """Both triangle-BVH builds: the host binned-SAH tree (default) and the
+    GPU Morton LBVH (RTPT_TRI_BUILD=lbvh, rt_lbvh.hip), same compact layout."""
+    if build == "lbvh":
+        monkeypatch.setenv("RTPT_TRI_BUILD", "lbvh")
     s = triangle_soup(40, 24, n, seed=n, dup=dup)
     assert s.describe()["lds_bytes"] == 0  # does not fit LDS: the BVH path
     sd = seed_splitmix(40, 24)
