@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 
 #include "../../include/rtpt.h"
 #include "rt_kernel.hpp"
@@ -723,7 +724,7 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
     for (uint32_t i = total; i-- > 0;)  // children are created after their parent
         if (!tree[i].count) size[i] = 1u + size[tree[i].left] + size[tree[i].right];
     nodes->assign((size_t)8 * total * 4, 0u);
-    for (uint32_t oct = 0; oct < 8; ++oct) {
+    auto emit_layout = [&](uint32_t oct) {
         uint32_t* L = nodes->data() + (size_t)oct * total * 4;
         // explicit-stack preorder: (node, entry index)
         std::vector<std::pair<uint32_t, uint32_t>> st;
@@ -752,6 +753,12 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
                 st.push_back({near, idx + 1});
             }
         }
+    };
+    {  // the 8 layouts are independent: one host thread each
+        std::vector<std::thread> th;
+        for (uint32_t oct = 1; oct < 8; ++oct) th.emplace_back(emit_layout, oct);
+        emit_layout(0);
+        for (auto& t : th) t.join();
     }
     sorted->resize(n);
     perm->resize(n);
