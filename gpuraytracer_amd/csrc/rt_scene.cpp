@@ -259,33 +259,6 @@ static float culling_margin(const rt_float3* verts, uint32_t n_tri, const Sphere
     return 4e-5f * ext;
 }
 
-// Which child a ray of direction octant `oct` (bit a: component a < 0) should
-// visit first.  kOrderAxis: the near side of the node's split axis.
-// kOrderCorner: the child whose box corner a ray of that octant enters
-// through is nearer along the octant's diagonal, sum_a s_a * (s_a > 0 ? lo_a :
-// hi_a) with s_a = -1 for a set bit -- all three axes, not only the split's.
-// Only speed depends on the order.
-enum BvhOrder { kOrderAxis = 0, kOrderCorner = 1 };
-static int bvh_order() {
-    static const int o = [] {
-        const char* v = getenv("RTPT_BVH_ORDER");  // tuning knob
-        return (v && !strcmp(v, "axis")) ? (int)kOrderAxis : (int)kOrderCorner;
-    }();
-    return o;
-}
-static double corner_key(const float lo[3], const float hi[3], int oct) {
-    double k = 0.0;
-    for (int a = 0; a < 3; ++a) k += ((oct >> a) & 1) ? -(double)hi[a] : (double)lo[a];
-    return k;
-}
-// true when the right child goes first for octant `oct`
-static bool right_first(int axis, const float* llo, const float* lhi, const float* rlo, const float* rhi,
-                        int oct) {
-    if (bvh_order() == kOrderAxis) return (oct >> axis) & 1;
-    const double kl = corner_key(llo, lhi, oct), kr = corner_key(rlo, rhi, oct);
-    return kr < kl || (kr == kl && ((oct >> axis) & 1));
-}
-
 // BVH over the spheres (median split of the centroids on the longest axis,
 // one sphere per leaf by default), emitted as 8 depth-first layouts, one per ray-direction
 // octant: at every inner node the child on the near side of the split for that
@@ -419,10 +392,9 @@ struct BvhBuild {
         if (n.count) {
             (*out)[me].leaf = (n.count << 24) | n.first;
         } else {
-            const Node &L = tree[n.left], &R = tree[n.right];
-            const bool rf = right_first(n.axis, L.lo, L.hi, R.lo, R.hi, oct);
-            emit(rf ? n.right : n.left, oct, out);
-            emit(rf ? n.left : n.right, oct, out);
+            const bool neg = (oct >> n.axis) & 1;  // moving toward lower coordinates
+            emit(neg ? n.right : n.left, oct, out);
+            emit(neg ? n.left : n.right, oct, out);
             (*out)[me].leaf = 0;
         }
         (*out)[me].escape = (uint32_t)out->size();
@@ -746,9 +718,8 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
                 w[3] = N.first | (N.count - 1u) << 24;  // leaf: first leaf-order triangle, count - 1
             } else {
                 w[3] = (oct * total + idx + size[v]) | 0x80000000u;
-                const Node &Lc = tree[N.left], &Rc = tree[N.right];
-                const bool rf = right_first(N.axis, Lc.lo, Lc.hi, Rc.lo, Rc.hi, (int)oct);
-                const uint32_t near = rf ? N.right : N.left, far = rf ? N.left : N.right;
+                const bool neg = (oct >> N.axis) & 1u;  // moving toward lower coordinates
+                const uint32_t near = neg ? N.right : N.left, far = neg ? N.left : N.right;
                 st.push_back({far, idx + 1 + size[near]});
                 st.push_back({near, idx + 1});
             }
