@@ -356,8 +356,17 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
 
 }  // namespace
 
-// lanes per pixel: 2 (20.3 ms per reference frame; 1 lane 26.1, 4 lanes 25.7)
-constexpr uint32_t kMisLanes = 2;
+// lanes per pixel: 3 (19.3 ms per reference frame: two rounds of the 6 camera
+// rays; 2 lanes 20.3, 6 lanes 19.8, 1 lane 26.1, 4 lanes 25.7)
+#ifndef RT_MIS_LANES
+#define RT_MIS_LANES 3
+#endif
+constexpr uint32_t kMisLanes = RT_MIS_LANES;
+// A wave holds 64 / ML pixels: an 8 x (8 / ML) tile when ML divides 8, else one
+// row of floor(64 / ML) pixels (the lanes past them leave at once); a
+// workgroup is 2 x 2 tiles or 1 x 4 rows.
+constexpr bool kMisTile = 8u % kMisLanes == 0;
+constexpr uint32_t kMisRowPixels = 64u / kMisLanes;
 // 7 waves/SIMD: 72 VGPRs without scratch since the primary hit, the pixel sum,
 // dl/dc and the running strategy sum wait in the per-lane LDS stash (round 2:
 // 120 VGPRs at 4 waves; 6 waves then spilled 54 VGPRs).  DESIGN.md §5
@@ -411,23 +420,30 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
     // ML lanes per pixel: lane `sub` traces the camera rays i = r*ML + sub of
     // round r, and the pixel's group leader adds the ML results to the pixel's
     // sum in ray order i (the same additions as one lane per pixel, :652-677).
-    // Twice the waves of one lane per pixel, each half as long: the 800x600
-    // frame's 7,500 one-lane waves filled the GPU's wave slots 1.8 times over,
-    // the second time only partly.
+    // More waves than one lane per pixel, each shorter: the 800x600 frame's
+    // 7,500 one-lane waves filled the GPU's wave slots 1.8 times over, the
+    // second time only partly.
     // Pixel of a lane; recomputed from an opaque threadIdx where it is used
     // (as in rt_kernel.hip), not held across the camera-ray loop.  A wave is
-    // 8 x (8 / ML) pixels, a workgroup 2 x 2 waves.
+    // 8 x (8 / ML) pixels (workgroup 2 x 2 waves) or a row of 64 / ML pixels
+    // (workgroup 4 rows).
     constexpr uint32_t ML = kMisLanes;
-    constexpr uint32_t kWY = 8u / ML;
+    constexpr uint32_t kWY = kMisTile ? 8u / ML : 1u;
     auto pixel_of = [&](uint32_t tid, uint32_t& x, uint32_t& j) {
         const uint32_t lane = tid & 63u, wave = tid >> 6, pix = lane / ML;
-        x = blockIdx.x * 16u + (wave & 1u) * 8u + (pix & 7u);
-        j = blockIdx.y * (2u * kWY) + (wave >> 1) * kWY + (pix >> 3);
+        if (kMisTile) {
+            x = blockIdx.x * 16u + (wave & 1u) * 8u + (pix & 7u);
+            j = blockIdx.y * (2u * kWY) + (wave >> 1) * kWY + (pix >> 3);
+        } else {
+            x = blockIdx.x * kMisRowPixels + pix;
+            j = blockIdx.y * 4u + wave;
+        }
     };
     {
         uint32_t x, j;
         pixel_of(threadIdx.x, x, j);
         if (x >= (uint32_t)P.W || j >= P.row_count) return;  // a pixel's ML lanes leave together
+        if (!kMisTile && (threadIdx.x & 63u) >= kMisRowPixels * ML) return;  // lanes past the row
     }
     const f3 cu{P.cam_u[0], P.cam_u[1], P.cam_u[2]}, cv{P.cam_v[0], P.cam_v[1], P.cam_v[2]};
     const f3 cw{P.cam_w[0], P.cam_w[1], P.cam_w[2]};
@@ -445,7 +461,7 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
     const uint32_t rounds = (P.camera_rays + ML - 1u) / ML;
     for (uint32_t r = 0; r < rounds; ++r) {  // :652
         const uint32_t tid = opaque_u32(threadIdx.x);
-        const uint32_t sub = tid % ML;
+        const uint32_t sub = (tid & 63u) % ML;  // ML need not divide 64
         const uint32_t i = r * ML + sub;
         f3 c{0.0f, 0.0f, 0.0f};
         bool has = false;  // Miss (:665), or a ray past camera_rays: nothing to add
@@ -492,7 +508,7 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
         if (ML == 1) {
             if (has) acc = acc + c;
         } else {  // in ray order: lane base + k holds ray r*ML + k
-            const int base = (int)((t2 & 63u) - t2 % ML);
+            const int base = (int)((t2 & 63u) - (t2 & 63u) % ML);
 #pragma unroll
             for (uint32_t k = 0; k < ML; ++k) {
                 const f3 ck{__shfl(c.x, base + (int)k), __shfl(c.y, base + (int)k),
@@ -509,7 +525,7 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
     const f3 acc{sv.xstash[6 * kBlockThreads + tl], sv.xstash[7 * kBlockThreads + tl],
                  sv.xstash[8 * kBlockThreads + tl]};
     const float nc = (float)P.camera_rays;
-    if (opaque_u32(threadIdx.x) % ML != 0) return;  // the group leader stores the pixel
+    if ((opaque_u32(threadIdx.x) & 63u) % ML != 0) return;  // the group leader stores the pixel
     uint32_t x, j;
     pixel_of(opaque_u32(threadIdx.x), x, j);
     const size_t o = (size_t)j * (size_t)P.W + x;
@@ -541,8 +557,8 @@ size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + sha
 // the global-memory kernel.
 template <int GEO>
 hipError_t launch_mis_g(const MisParams& P, size_t lds, hipStream_t stream) {
-    constexpr uint32_t TY = 2u * (8u / kMisLanes);  // workgroup: 16 x TY pixels
-    const dim3 grid((P.W + 15u) / 16u, (P.row_count + TY - 1) / TY);
+    constexpr uint32_t TX = kMisTile ? 16u : kMisRowPixels, TY = kMisTile ? 2u * (8u / kMisLanes) : 4u;
+    const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);  // workgroup: TX x TY pixels
     if (lds > 65536) {
         const hipError_t e = hipFuncSetAttribute((const void*)mis_kernel<GEO>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

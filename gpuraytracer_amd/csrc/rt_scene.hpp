@@ -37,7 +37,7 @@ struct PairIsect {
 struct TriShade {
     float s[16];
 };
-// Sphere intersection record, 16 B, staged in LDS: (c.xyz, r*r)
+// Sphere intersection record, 16 B, in BVH leaf order (read from global memory): (c.xyz, r*r)
 struct SphIsect {
     float q[4];
 };
@@ -98,12 +98,13 @@ struct CompiledScene {
     uint32_t sph_layout_nodes = 0;
     uint32_t sph_lds_entries = 0;       // entries per layout of sph_lds (a leaf of c spheres: c)
     std::vector<SphShade> sph_shade;    // by sphere id
-    // Compact sphere BVH for LDS: the layouts of octants
-    // (+,+,+) and (-,-,-), 16 B per entry: inner node = fp16 box (lo rounded
-    // down, hi up) + (escape | 0x80000000); leaf (one sphere) = (c.xyz, r*r)
-    // fp32, its sphere id in sph_lds_id.  Empty when the tree does not qualify.
-    std::vector<uint32_t> sph_lds;      // 2 layouts x sph_lds_entries x 4 words
-    std::vector<uint16_t> sph_lds_id;   // 2 layouts x sph_lds_entries
+    // Compact sphere BVH: one layout per direction octant,
+    // 16 B per entry: inner node = fp16 near/far box (lo rounded down, hi up;
+    // the plane a ray of the layout's octant enters through in the first
+    // slot) + (escape | 0x80000000); leaf (one sphere) = (c.xyz, r*r) fp32,
+    // its sphere id in sph_lds_id.  Empty when the tree does not qualify.
+    std::vector<uint32_t> sph_lds;      // 8 layouts x sph_lds_entries x 4 words
+    std::vector<uint16_t> sph_lds_id;   // 8 layouts x sph_lds_entries
     // Box clusters over the pair records: 28 floats each,
     // (u0.xyz, lo0) (u1.xyz, lo1) (u2.xyz, lo2) (hi0, hi1, hi2, flags)
     // (m0, m1, m2, m3) (m4, m5, all, 0) (w0, w1, w2, 0): an oriented box (padded
