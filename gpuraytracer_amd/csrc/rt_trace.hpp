@@ -199,8 +199,10 @@ struct RayBox {
     f3 invd, oinv;
 };
 
+// 1/v clamped to +-1e20 (v = +-0 gives +-1e20): one v_rcp + one v_med3.
+// Feeds only conservative slab tests (speed, not results, depends on it).
 __device__ __forceinline__ float safe_rcp(float v) {
-    return __builtin_amdgcn_rcpf(fabsf(v) < 1e-20f ? copysignf(1e-20f, v) : v);
+    return __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(v), -1e20f, 1e20f);
 }
 
 __device__ __forceinline__ RayBox ray_box(f3 o, f3 d) {
@@ -626,7 +628,7 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
         }
         const float tlo0 = vmax3(en[0], en[1], vmax(en[2], tmin));
         const float thi0 = vmin3(ex[0], ex[1], vmin(ex[2], tmax));
-        const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
+        const float tlo = fmaf(-kEps, fabsf(tlo0), tlo0), thi = fmaf(kEps, fabsf(thi0), thi0);  // kEps*|x| is exact: the same values
         if (!__builtin_amdgcn_ballot_w64(tlo <= thi)) continue;  // no lane meets the box
         const uint32_t m[6] = {__float_as_uint(M0.x), __float_as_uint(M0.y), __float_as_uint(M0.z),
                                __float_as_uint(M0.w), __float_as_uint(M1.x), __float_as_uint(M1.y)};
@@ -668,7 +670,7 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
             tlo0 = vmax(tlo0, vmin(t0, t1));
             thi0 = vmin(thi0, vmax(t0, t1));
         }
-        const float tlo = tlo0 - kEps * fabsf(tlo0), thi = thi0 + kEps * fabsf(thi0);
+        const float tlo = fmaf(-kEps, fabsf(tlo0), tlo0), thi = fmaf(kEps, fabsf(thi0), thi0);  // kEps*|x| is exact: the same values
         mask |= (tlo <= thi) ? __float_as_uint(r[5].z) : 0u;
     }
     return mask;
