@@ -976,10 +976,28 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
             return f;
         };
         for (int a = 0; a < 3; ++a) {
-            cl.push_back((float)best.u[a].x);
-            cl.push_back((float)best.u[a].y);
-            cl.push_back((float)best.u[a].z);
-            cl.push_back((float)(best.lo[a] - pad[a]));
+            const float lo_f = (float)(best.lo[a] - pad[a]), hi_f = (float)(best.hi[a] + pad[a]);
+            if (flags & 8u) {
+                // A container's axes are world axes, so the kernel reads no axis
+                // vector: (x, y) hold the box shrunk past each face plane by the
+                // normal tolerance plus a 2^-16 relative slack on the bounds and
+                // on the largest |coordinate| inside the box (rt_trace.hpp,
+                // cluster_candidates<SEG>: a segment end outside the box fails
+                // the test anyway, one inside it has |e| <= M).  Float operations
+                // in the kernel's order.
+                const float wf = (float)(pad[a] + tol_n), kEps = 1.52587890625e-05f;
+                const float M = fmaxf(fabsf(lo_f), fabsf(hi_f));
+                const float in_lo = (lo_f + wf) + kEps * (fabsf(lo_f) + M);
+                const float in_hi = (hi_f - wf) - kEps * (fabsf(hi_f) + M);
+                cl.push_back(in_lo);
+                cl.push_back(in_hi);
+                cl.push_back(0.0f);
+            } else {
+                cl.push_back((float)best.u[a].x);
+                cl.push_back((float)best.u[a].y);
+                cl.push_back((float)best.u[a].z);
+            }
+            cl.push_back(lo_f);
         }
         cl.push_back((float)(best.hi[0] + pad[0]));
         cl.push_back((float)(best.hi[1] + pad[1]));

@@ -565,7 +565,8 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
 // a box with volume, e.g. the room) is skipped for the whole wave when every
 // lane's segment [o, o + d*tmax] lies inside the box shrunk to more than the
 // normal tolerance from each face plane: the box is convex, so the segment
-// stays away from every face and no face can accept a hit.
+// stays away from every face and no face can accept a hit.  The shrunk box
+// is precomputed on the host into the container's unused axis slots.
 template <bool SEG = false>
 __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o, f3 d, float tmin,
                                                        float tmax) {
@@ -577,21 +578,13 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
         const f3 e = o + d * tmax;
         for (uint32_t c = 0; c < sv.nC; ++c) {
             const float4* r = sv.clu + kCluF4 * c;
-            const float4 H = r[3];
-            if (!(__float_as_uint(H.w) & 8u)) continue;
-            const float4 W = r[6];
-            const float lo[3] = {r[0].w, r[1].w, r[2].w}, hi[3] = {H.x, H.y, H.z};
-            const float wf[3] = {W.x, W.y, W.z};
-            const float oo[3] = {o.x, o.y, o.z}, ee[3] = {e.x, e.y, e.z};
-            bool inside = true;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                // lo' + w = face plane + tol_n; 2^-16 relative slack for the
-                // rounding of o + d*tmax and of the bounds
-                const float in_lo = lo[a] + wf[a] + kEps * (fabsf(lo[a]) + fabsf(ee[a]));
-                const float in_hi = hi[a] - wf[a] - kEps * (fabsf(hi[a]) + fabsf(ee[a]));
-                inside = inside && oo[a] > in_lo && oo[a] < in_hi && ee[a] > in_lo && ee[a] < in_hi;
-            }
+            if (!(__float_as_uint(r[3].w) & 8u)) continue;
+            // the shrunk box (rt_scene.cpp): lo' + w = face plane + tol_n, with a
+            // 2^-16 relative slack for the rounding of o + d*tmax and of the bounds
+            const float4 X = r[0], Y = r[1], Z = r[2];
+            const bool inside = o.x > X.x && o.x < X.y && e.x > X.x && e.x < X.y &&
+                                o.y > Y.x && o.y < Y.y && e.y > Y.x && e.y < Y.y &&
+                                o.z > Z.x && o.z < Z.y && e.z > Z.x && e.z < Z.y;
             if (__builtin_amdgcn_ballot_w64(!inside) == 0) skip |= 1u << c;
         }
     }
