@@ -170,9 +170,17 @@ __device__ __forceinline__ MisMat hit_m(const SceneView& sv, const MisHit& x) {
     return load_mat(sv.shade + 3 * x.id);
 }
 
-template <int GEO>
+// SEG (the light queries, tmax = distance to the light sample): with box
+// clusters the room is skipped for waves whose segments stay inside it -- a
+// hit beyond tmax is no hit, and none of the room's faces can be hit before.
+template <int GEO, bool SEG = false>
 __device__ __forceinline__ int mis_closest(const SceneView& sv, f3 o, f3 d, float tmax, float* t) {
     *t = tmax;
+    if (GEO == kGeoPairClu && SEG) {
+        int id = -1;
+        cluster_query<false, true>(sv, o, d, 0.001f, t, &id);
+        return id;
+    }
     return closest_hit<GEO, false, true, 0>(sv, o, d, 0.001f, t);
 }
 
@@ -250,7 +258,7 @@ __device__ __forceinline__ f3 direct_light(const MisParams& P, const SceneView& 
         }
     }
     float t;
-    const int id = mis_closest<GEO>(sv, origin, L, dist, &t);
+    const int id = mis_closest<GEO, true>(sv, origin, L, dist, &t);
     if (id < 0 || sv.shade[3 * id].w == 0.0f) return f3{0.0f, 0.0f, 0.0f};  // not HitLight
     return contrib;
 }

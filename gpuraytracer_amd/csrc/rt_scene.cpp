@@ -979,16 +979,22 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
             const float lo_f = (float)(best.lo[a] - pad[a]), hi_f = (float)(best.hi[a] + pad[a]);
             if (flags & 8u) {
                 // A container's axes are world axes, so the kernel reads no axis
-                // vector: (x, y) hold the box shrunk past each face plane by the
-                // normal tolerance plus a 2^-16 relative slack on the bounds and
-                // on the largest |coordinate| inside the box (rt_trace.hpp,
-                // cluster_candidates<SEG>: a segment end outside the box fails
-                // the test anyway, one inside it has |e| <= M).  Float operations
-                // in the kernel's order.
-                const float wf = (float)(pad[a] + tol_n), kEps = 1.52587890625e-05f;
+                // vector: (x, y) hold the box shrunk past each face plane by
+                // tol_seg (rt_trace.hpp, cluster_candidates<SEG>: a segment that
+                // stays that far inside cannot have an accepted hit on a face).
+                // The face triangles lie within tol of the plane; an exact
+                // crossing outside (0, tmax) shows up inside it only through the
+                // rounding of t, a few 2^-24 of the distance to the plane
+                // (< 2 ext): 1e-6 of the scene extent covers it 10x over.  Then a
+                // 2^-20 relative slack on the bounds and on the largest
+                // |coordinate| inside the box for the rounding of the bound and
+                // of e = o + d*tmax (a segment end outside the box fails the
+                // test anyway, one inside it has |e| <= M).
+                const double tol_seg = tol + 1e-6 * fmax(ext, cam_ext);
+                const float kSlack = 9.5367431640625e-07f;  // 2^-20
                 const float M = fmaxf(fabsf(lo_f), fabsf(hi_f));
-                const float in_lo = (lo_f + wf) + kEps * (fabsf(lo_f) + M);
-                const float in_hi = (hi_f - wf) - kEps * (fabsf(hi_f) + M);
+                const float in_lo = (float)(best.lo[a] + tol_seg) + kSlack * (fabsf(lo_f) + M);
+                const float in_hi = (float)(best.hi[a] - tol_seg) - kSlack * (fabsf(hi_f) + M);
                 cl.push_back(in_lo);
                 cl.push_back(in_hi);
                 cl.push_back(0.0f);

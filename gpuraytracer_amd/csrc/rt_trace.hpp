@@ -579,8 +579,8 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
         for (uint32_t c = 0; c < sv.nC; ++c) {
             const float4* r = sv.clu + kCluF4 * c;
             if (!(__float_as_uint(r[3].w) & 8u)) continue;
-            // the shrunk box (rt_scene.cpp): lo' + w = face plane + tol_n, with a
-            // 2^-16 relative slack for the rounding of o + d*tmax and of the bounds
+            // the shrunk box (rt_scene.cpp): face plane + tol_seg, with a 2^-20
+            // relative slack for the rounding of o + d*tmax and of the bounds
             const float4 X = r[0], Y = r[1], Z = r[2];
             const bool inside = o.x > X.x && o.x < X.y && e.x > X.x && e.x < X.y &&
                                 o.y > Y.x && o.y < Y.y && e.y > Y.x && e.y < Y.y &&
@@ -703,14 +703,16 @@ __device__ __forceinline__ void pair_test_rank(const float4* r, uint32_t k, f3 o
 // unclustered pairs by every lane (wave-uniform records, LDS broadcast), then
 // each lane's own candidate pairs (per-lane LDS reads).  For ANY, *best is
 // tmax and is not changed.
-template <bool ANY>
+// SEG: skip containers the wave's segments [o, o + d*tmax] stay inside (any
+// hit, and the MIS light queries: closest hits that only matter up to tmax).
+template <bool ANY, bool SEG = ANY>
 __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, float tmin,
                                               float* best, int* id) {
     for (uint32_t free = sv.pair_free; free != 0u; free &= free - 1u) {
         const uint32_t k = (uint32_t)__builtin_ctz(free);
         pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);
     }
-    uint32_t cand = cluster_candidates<ANY>(sv, o, d, tmin, *best);
+    uint32_t cand = cluster_candidates<SEG>(sv, o, d, tmin, *best);
     RT_STAT(12, 1);
     RT_STAT(15, __popcll(__ballot(1)));
     while (cand != 0u && !(ANY && *id >= 0)) {
