@@ -49,13 +49,14 @@ def main(argv=None):
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--quads", default="0,19", help="extra planar quads per case")
     a = ap.parse_args(argv)
     import gpuraytracer_amd as g
     from gpuraytracer_amd import Renderer, RenderParams, Scene, seed_splitmix
     base = Scene.cornell_box(a.width, a.height)
     sph = Scene.random_spheres(a.width, a.height, a.spheres, seed=42).spheres
     sd = seed_splitmix(a.width, a.height, key=42)
-    for n_quads in (0, 19):
+    for n_quads in [int(q) for q in a.quads.split(",")]:
         if n_quads:
             mats, verts = with_quads(g, base, n_quads)
             s = Scene(base.camera, mats, verts, base.light, sph)
