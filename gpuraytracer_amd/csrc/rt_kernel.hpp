@@ -22,9 +22,12 @@ constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padde
 // 1024 threads 186.1 ms, 512 177.9, 256 162.1, 128 160.5, 64 158.4).  Every
 // workgroup stages its own copy of the pair records, so the kernel is taken
 // only while they are small (kSphPairLdsMaxBytes; config 4: 672 B): above it
-// the pair kernel with the 32-B-node sphere walks serves the scene.
+// the pair kernel with the 32-B-node sphere walks serves the scene.  Measured
+// on Cornell + 1000 spheres + extra quads, 1080p x 64 spp (tools/bench_mixed.py,
+// one-wave vs pair kernel): 37 pairs 47.9 vs 66.7 ms, 48 pairs 59.5 vs 69.4,
+// 58 pairs 71.8 vs 71.7, 68 pairs 84.8 vs 73.0: the crossover is ~6.5 KB.
 constexpr uint32_t kSphBlockThreads = 64;
-constexpr size_t kSphPairLdsMaxBytes = 4 * 1024;
+constexpr size_t kSphPairLdsMaxBytes = 6 * 1024;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
 // Layouts of the triangle BVH (rt_scene.cpp build_tri_sah / rt_lbvh.hip,
 // rt_trace.hpp tri_cbvh_*): one per direction octant, 16 B per node.

@@ -130,20 +130,20 @@ def _with_quads(base, n_quads, seed=3):
 
 def test_sphere_kernel_pair_budget():
     """The one-wave sphere kernel stages the pair records in every workgroup, so
-    it is taken only while they fit kSphPairLdsMaxBytes (4 KB, rt_kernel.hpp);
+    it is taken only while they fit kSphPairLdsMaxBytes (6 KB, rt_kernel.hpp);
     above it the pair kernel (records shared by 256 threads) serves the scene."""
     base = g.Scene.cornell_box(64, 48)
     sph = g.Scene.random_spheres(64, 48, 200).spheres
     mixed = g.Scene(base.camera, base.materials, base.vertices, base.light, sph)
     info = mixed.describe()
     assert info["n_triangle_pairs"] == 18 and info["sphere_kernel_lds_bytes"] == 18 * 112
-    mats, verts = _with_quads(base, 18)  # 36 pairs = 4032 B: still the sphere kernel
+    mats, verts = _with_quads(base, 36)  # 54 pairs = 6048 B: still the sphere kernel
     at = g.Scene(base.camera, mats, verts, base.light, sph).describe()
-    assert at["n_triangle_pairs"] == 36 and at["sphere_kernel_lds_bytes"] == 36 * 112
-    mats, verts = _with_quads(base, 19)  # 37 pairs = 4144 B > 4 KB
+    assert at["n_triangle_pairs"] == 54 and at["sphere_kernel_lds_bytes"] == 54 * 112
+    mats, verts = _with_quads(base, 37)  # 55 pairs = 6160 B > 6 KB
     over = g.Scene(base.camera, mats, verts, base.light, sph).describe()
-    assert over["n_triangle_pairs"] == 37 and over["sphere_kernel_lds_bytes"] == 0
-    assert over["lds_bytes"] == 37 * 112
+    assert over["n_triangle_pairs"] == 55 and over["sphere_kernel_lds_bytes"] == 0
+    assert over["lds_bytes"] == 55 * 112
 
 
 def test_portrait_resolution_is_rejected():

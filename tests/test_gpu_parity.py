@@ -261,13 +261,13 @@ def test_spheres_16_lanes_frame_and_rows_bit_exact_vs_oracle():
 
 def test_mixed_scene_sphere_kernel_and_pair_fallback_bit_exact():
     """Cornell box (36 triangles, both boxes) + 300 spheres: the one-wave sphere
-    kernel; with 19 more quads (37 pairs, over the 4 KB per-workgroup budget) the
+    kernel; with 37 more quads (55 pairs, over the 6 KB per-workgroup budget) the
     pair kernel with the 32-B-node sphere walks.  Both are the oracle."""
     from test_abi import _with_quads
     base = Scene.cornell_box(48, 32)
     sph = Scene.random_spheres(48, 32, 300, seed=21).spheres
     sd = seed_splitmix(48, 32, key=21)
-    for n_quads, sphere_kernel in ((0, True), (19, False)):
+    for n_quads, sphere_kernel in ((0, True), (36, True), (37, False)):
         if n_quads:
             mats, verts = _with_quads(base, n_quads)
             s = Scene(base.camera, mats, verts, base.light, sph)

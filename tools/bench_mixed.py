@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Mixed-scene timing: the Cornell box with both boxes (36
 triangles, 18 pair records, 2 KB) plus N random spheres takes the one-wave
-sphere kernel; with extra planar quads past the 4 KB per-workgroup pair budget
+sphere kernel; with extra planar quads past the 6 KB per-workgroup pair budget
 it falls back to the pair kernel with the 32-B-node sphere walks.  Prints one
 JSON line per case: kernel, kernel ms, Msamples/s.
 
@@ -49,7 +49,7 @@ def main(argv=None):
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--quads", default="0,19", help="extra planar quads per case")
+    ap.add_argument("--quads", default="0,36,37", help="extra planar quads per case")
     a = ap.parse_args(argv)
     import gpuraytracer_amd as g
     from gpuraytracer_amd import Renderer, RenderParams, Scene, seed_splitmix
