@@ -469,3 +469,31 @@ def test_lanes_per_pixel_and_interleaved_rows_bit_exact(lanes, monkeypatch):
     ref = oracle_lib.render(s, sd, 19, 3)
     assert_parity(full, ref, "lanes" + lanes)
     assert_parity(tile, ref[2::5], "tile lanes" + lanes)
+
+
+@pytest.mark.parametrize("mem", [None, "bvh", "spheres"])
+def test_zero_light_terms_black_materials_bit_exact(mem, monkeypatch):
+    """Lanes whose light term is exactly 0 skip their shadow query (DESIGN.md
+    §3.14): black boxes and a black wall make whole paths carry a zero
+    throughput (every later light term is 0), and the ceiling and the light's
+    back side give zero terms on lit materials.  Box clusters, the triangle BVH
+    (bounce 0 on wave packets, which keep the query) and the sphere kernel
+    (half the spheres black)."""
+    s = Scene.cornell_box(48, 32)
+    mats = s.materials
+    for k in list(range(0, 2)) + list(range(10, 34)):  # a wall and both boxes
+        mats[k].diffuse.x = mats[k].diffuse.y = mats[k].diffuse.z = 0.0
+    sph = None
+    if mem == "spheres":
+        sph = Scene.random_spheres(48, 32, 300, seed=5).spheres
+        for k in range(0, 300, 2):
+            m = sph[k].material
+            m.diffuse.x = m.diffuse.y = m.diffuse.z = 0.0
+    elif mem == "bvh":
+        monkeypatch.setenv("RTPT_SCENE_MEM", "bvh")
+    scene = Scene(s.camera, mats, s.vertices, s.light, sph)
+    sd = seed_splitmix(48, 32, key=9)
+    with Renderer(scene, seeds=sd) as r:
+        out = r.render(RenderParams(spp=4, bounces=3))
+    assert_parity(out, oracle_lib.render(scene, sd, 4, 3), f"black materials {mem}")
+    assert np.isfinite(out).all()
