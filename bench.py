@@ -118,8 +118,8 @@ class CudaBackend:
         self.local = local
 
     def renderer(self, scene):
-        from gpuraytracer_amd import Renderer
-        return Renderer(scene, device=self.local)
+        from gpuraytracer_amd import Options, Renderer
+        return Renderer(scene, device=self.local, options=Options.from_env())
 
     def comm_unique_id(self) -> bytes:
         from gpuraytracer_amd import comm_unique_id

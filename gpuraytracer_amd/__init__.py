@@ -18,7 +18,7 @@ from __future__ import annotations
 
 from ._native import (ABI_VERSION, CameraGPU, MaterialGPU, RtError, SphereGPU,
                       SquareLightGPU, float3, lib, library_path)
-from .host import (DEFAULT_SEED_KEY, MisParams, RenderParams, Renderer, Scene, comm_unique_id,
+from .host import (DEFAULT_SEED_KEY, MisParams, Options, RenderParams, Renderer, Scene, comm_unique_id,
                    place_tiles_host, seed_splitmix, tile_layout, tonemap_rgba8)
 
 __all__ = [

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTPT_LIB overrides the in-tree library (A/B builds of the kernel).
 library_path = os.environ.get("RTPT_LIB") or os.path.join(_HERE, "librtpt.so")
@@ -91,6 +91,21 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
                  "sphere_kernel_lds_bytes")]
 
 
+class CreateOptions(ctypes.Structure):  # rt_create_options
+    _fields_ = [("scene_layout", ctypes.c_uint32), ("lanes_per_pixel", ctypes.c_uint32),
+                ("tri_bvh_build", ctypes.c_uint32), ("tri_leaf_max", ctypes.c_uint32),
+                ("tri_leaf_cost", ctypes.c_float), ("sphere_leaf_max", ctypes.c_uint32),
+                ("sphere_median", ctypes.c_uint32), ("walk_scheduler", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 8)]
+
+
+assert ctypes.sizeof(CreateOptions) == 64
+
+# rt_scene_layout / rt_tri_bvh_build / rt_walk_scheduler (include/rtpt.h)
+LAYOUTS = {"auto": 0, "pairs": 1, "single": 2, "global": 3, "smem": 3, "pairsmem": 4, "sorted": 5, "bvh": 6}
+TRI_BUILDS = {"default": 0, "host": 1, "lbvh": 2, "gpusah": 3}
+WALKS = {"auto": 0, "lockstep": 1, "free": 2}
+
 RT_OK = 0
 RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE, RT_KEEP_SUM, RT_OUT_RGBA8 = 0x1, 0x2, 0x4, 0x8, 0x10
 RT_MAX_BOUNCES = 4
@@ -123,6 +138,9 @@ class MisParamsC(ctypes.Structure):  # rt_mis_params
 _P = ctypes.c_void_p
 SIGNATURES = {
     "rt_create": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(_P)]),
+    "rt_create_ex": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(CreateOptions),
+                                    ctypes.POINTER(_P)]),
+    "rt_create_options_default": (None, [ctypes.POINTER(CreateOptions)]),
     "rt_set_seeds": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32]),
     "rt_fill_seeds": (ctypes.c_int, [_P, ctypes.c_uint64]),
     "rt_render": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P]),
@@ -167,6 +185,8 @@ SIGNATURES = {
                                                 ctypes.POINTER(ctypes.c_uint32)]),
     "rt_tonemap_rgba8": (None, [_P, ctypes.c_size_t, _P]),
     "rt_scene_describe": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(SceneInfo)]),
+    "rt_scene_describe_ex": (ctypes.c_int, [ctypes.POINTER(SceneDesc), ctypes.POINTER(CreateOptions),
+                                            ctypes.POINTER(SceneInfo)]),
 }
 
 

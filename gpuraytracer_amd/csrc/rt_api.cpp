@@ -37,7 +37,7 @@ struct rt_ctx {
     float4* d_sph_nodes = nullptr;
     uint32_t* d_sph_perm = nullptr;
     uint4* d_tri_nodes = nullptr;    // triangle BVH: 8 compact layouts (build_tri_sah / rt_lbvh.hip)
-    bool tri_lbvh = false;           // RTPT_TRI_BUILD=lbvh: GPU Morton LBVH instead of the host SAH build
+    uint32_t tri_build = RT_TRI_BVH_HOST_SAH;  // rt_create_options.tri_bvh_build (resolved)
     float4* d_tri_sorted = nullptr;
     uint32_t* d_tri_perm = nullptr;
     uint32_t tri_bvh_nodes = 0;      // per layout
@@ -68,12 +68,16 @@ struct rt_ctx {
     size_t gather_cap = 0;
     hipEvent_t ev_tiles = nullptr;  // end of the last gather's reads of d_tile / d_gather
     bool tiles_pending = false;
-    uint32_t lanes = 0;  // RTPT_LANES=1|4|16: lanes per pixel (tuning knob; 0 = auto)
-    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // RTPT_SCENE_MEM=single|smem|pairsmem|sorted|bvh (tuning knob)
+    uint32_t lanes = 0;  // rt_create_options.lanes_per_pixel (0 = auto)
+    rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // rt_create_options.scene_layout
+    uint32_t walk = 0;   // rt_create_options.walk_scheduler
     std::string err;
 };
 
 namespace {
+
+// RT_TRI_BVH_DEFAULT resolves to this build
+constexpr uint32_t kDefaultTriBuild = RT_TRI_BVH_HOST_SAH;
 
 thread_local std::string g_create_err = "no error";
 
@@ -262,6 +266,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.samples_total = (uint32_t)total;
     K.flags = ((p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u) | ((p->flags & RT_OUT_RGBA8) ? rt::kOutRgba8 : 0u);
     K.lanes = c->lanes;
+    K.walk = c->walk;
     {
         const uint64_t imax = (uint64_t)c->seed_max + p->sample_base + (p->spp ? p->spp - 1u : 0u);
         K.max_index = imax > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)imax;
@@ -553,9 +558,66 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
     return RT_OK;
 }
 
+// rt_create_options (include/rtpt.h) -> the context's choices and the host
+// builds' options.  False (with *why) for a value outside its range.
+struct Resolved {
+    uint32_t lanes = 0, tri_build = RT_TRI_BVH_HOST_SAH, walk = RT_WALK_AUTO;
+    rt::SceneMem mem = rt::SceneMem::kAuto;
+    uint32_t tri_leaf_max = rt::kTriLeafMax;
+    double tri_leaf_cost = 1.0;
+    rt::BuildOptions build;
+};
+
+bool resolve_options(const rt_create_options* o, Resolved* r, const char** why) {
+    *r = Resolved();
+    if (!o) return true;
+    for (uint32_t v : o->reserved)
+        if (v != 0) { *why = "rt_create_options.reserved must be zero"; return false; }
+    switch (o->scene_layout) {
+        case RT_LAYOUT_AUTO: r->mem = rt::SceneMem::kAuto; break;
+        case RT_LAYOUT_PAIRS: r->mem = rt::SceneMem::kPairLds; break;
+        case RT_LAYOUT_SINGLE: r->mem = rt::SceneMem::kLdsSingle; break;
+        case RT_LAYOUT_GLOBAL: r->mem = rt::SceneMem::kSmem; break;
+        case RT_LAYOUT_PAIRS_SMEM: r->mem = rt::SceneMem::kPairSmem; break;
+        case RT_LAYOUT_SORTED: r->mem = rt::SceneMem::kPairSorted; break;
+        case RT_LAYOUT_BVH: r->mem = rt::SceneMem::kTriBvh; break;
+        default: *why = "rt_create_options.scene_layout out of range"; return false;
+    }
+    if (o->lanes_per_pixel != 0 && o->lanes_per_pixel != 1 && o->lanes_per_pixel != 4 &&
+        o->lanes_per_pixel != 16) {
+        *why = "rt_create_options.lanes_per_pixel must be 0, 1, 4 or 16";
+        return false;
+    }
+    r->lanes = o->lanes_per_pixel;
+    switch (o->tri_bvh_build) {
+        case RT_TRI_BVH_DEFAULT: r->tri_build = kDefaultTriBuild; break;
+        case RT_TRI_BVH_HOST_SAH: case RT_TRI_BVH_GPU_LBVH:
+            r->tri_build = o->tri_bvh_build; break;
+        default: *why = "rt_create_options.tri_bvh_build out of range"; return false;
+    }
+    if (o->tri_leaf_max > 128) { *why = "rt_create_options.tri_leaf_max must be <= 128"; return false; }
+    if (o->tri_leaf_max) r->tri_leaf_max = o->tri_leaf_max;
+    if (!(o->tri_leaf_cost >= 0.0f) || o->tri_leaf_cost > 1e6f) {
+        *why = "rt_create_options.tri_leaf_cost must be in [0, 1e6]";
+        return false;
+    }
+    if (o->tri_leaf_cost > 0.0f) r->tri_leaf_cost = o->tri_leaf_cost;
+    if (o->sphere_leaf_max > 255) { *why = "rt_create_options.sphere_leaf_max must be <= 255"; return false; }
+    if (o->sphere_leaf_max) r->build.sphere_leaf_max = o->sphere_leaf_max;
+    if (o->sphere_median > 1) { *why = "rt_create_options.sphere_median must be 0 or 1"; return false; }
+    r->build.sphere_sah = o->sphere_median == 0;
+    if (o->walk_scheduler > RT_WALK_FREE) { *why = "rt_create_options.walk_scheduler out of range"; return false; }
+    r->walk = o->walk_scheduler;
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+void rt_create_options_default(rt_create_options* opt) {
+    if (opt) memset(opt, 0, sizeof(*opt));
+}
 
 int rt_abi_version(void) { return RTPT_ABI_VERSION; }
 
@@ -576,13 +638,18 @@ const char* rt_last_error(const rt_ctx* ctx) {
     return ctx ? ctx->err.c_str() : g_create_err.c_str();
 }
 
-int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
+int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) { return rt_create_ex(d, nullptr, out_ctx); }
+
+int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** out_ctx) {
     if (!out_ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "out_ctx is null");
     *out_ctx = nullptr;
     if (!d) return fail(nullptr, RT_ERR_INVALID_ARG, "scene desc is null");
     if (!d->camera) return fail(nullptr, RT_ERR_INVALID_ARG, "camera is null");
     if (!d->square_lights || d->n_square_lights < 1)
         return fail(nullptr, RT_ERR_INVALID_ARG, "square_lights[0] is required (raytrace.metal:22)");
+    Resolved ro;
+    const char* why = nullptr;
+    if (!resolve_options(opt, &ro, &why)) return fail(nullptr, RT_ERR_INVALID_ARG, why);
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
     if (e != hipSuccess || count <= 0)
@@ -594,20 +661,14 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return fail(nullptr, RT_ERR_OUT_OF_MEMORY, "host allocation");
     c->device = d->device;
-    if (const char* m = getenv("RTPT_LANES")) c->lanes = (uint32_t)atoi(m);
-    if (const char* m = getenv("RTPT_TRI_BUILD")) c->tri_lbvh = !strcmp(m, "lbvh");  // tuning knob
-    if (const char* m = getenv("RTPT_SCENE_MEM")) {
-        if (!strcmp(m, "single")) c->scene_mem = rt::SceneMem::kLdsSingle;
-        if (!strcmp(m, "smem")) c->scene_mem = rt::SceneMem::kSmem;
-        if (!strcmp(m, "sorted")) c->scene_mem = rt::SceneMem::kPairSorted;
-        if (!strcmp(m, "pairs")) c->scene_mem = rt::SceneMem::kPairLds;
-        if (!strcmp(m, "pairsmem")) c->scene_mem = rt::SceneMem::kPairSmem;
-        if (!strcmp(m, "bvh")) c->scene_mem = rt::SceneMem::kTriBvh;
-    }
+    c->lanes = ro.lanes;
+    c->tri_build = ro.tri_build;
+    c->scene_mem = ro.mem;
+    c->walk = ro.walk;
     DeviceGuard g(c->device);
     const char* err = nullptr;
     if (!rt::compile_scene(*d->camera, d->materials, d->vertices, d->n_triangles,
-                           d->square_lights[0], d->spheres, d->n_spheres, &c->scene, &err)) {
+                           d->square_lights[0], d->spheres, d->n_spheres, &c->scene, &err, ro.build)) {
         delete c;
         return fail(nullptr, RT_ERR_INVALID_ARG, err);
     }
@@ -647,7 +708,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
                                            std::min(lds_pairs, lds_single) > rt::kMaxLdsBytes)));
         if (need_bvh) {
             const size_t nn = 2 * (size_t)nT - 1;
-            if (c->tri_lbvh) {  // GPU build (rt_lbvh.hip)
+            if (c->tri_build == RT_TRI_BVH_GPU_LBVH) {  // GPU Morton build (rt_lbvh.hip)
                 if ((e = hipMalloc((void**)&c->d_tri_nodes, rt::kTriCompactLayouts * nn * sizeof(uint4))) != hipSuccess ||
                     (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
                     (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
@@ -661,7 +722,8 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
             } else {  // host binned SAH (rt_scene.cpp build_tri_sah), uploaded
                 std::vector<uint32_t> nodes, perm;
                 std::vector<rt::TriIsect> sorted;
-                if (!rt::build_tri_sah(s.tri_isect, s.margin, &nodes, &sorted, &perm)) {
+                if (!rt::build_tri_sah(s.tri_isect, s.margin, &nodes, &sorted, &perm, ro.tri_leaf_max,
+                                       ro.tri_leaf_cost)) {
                     status = RT_ERR_INVALID_ARG; msg = "triangle BVH build: too many triangles (2^24)"; break;
                 }
                 if ((e = upload(&c->d_tri_nodes, nodes.data(), nodes.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
@@ -671,7 +733,7 @@ int rt_create(const rt_scene_desc* d, rt_ctx** out_ctx) {
                 }
                 c->tri_bvh_nodes = (uint32_t)(nodes.size() / (4 * rt::kTriCompactLayouts));
             }
-            if (c->tri_lbvh) c->tri_bvh_nodes = (uint32_t)nn;
+            if (c->tri_build == RT_TRI_BVH_GPU_LBVH) c->tri_bvh_nodes = (uint32_t)nn;
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
         if ((e = hipMalloc((void**)&c->d_seeds, npx * sizeof(uint32_t))) != hipSuccess) {
@@ -860,12 +922,19 @@ int rt_destroy(rt_ctx* c) {
 }
 
 int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
+    return rt_scene_describe_ex(d, nullptr, info);
+}
+
+int rt_scene_describe_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_scene_info* info) {
     if (!d || !info || !d->camera || !d->square_lights)
         return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
+    Resolved ro;
+    const char* why = nullptr;
+    if (!resolve_options(opt, &ro, &why)) return fail(nullptr, RT_ERR_INVALID_ARG, why);
     rt::CompiledScene s;
     const char* err = nullptr;
     if (!rt::compile_scene(*d->camera, d->materials, d->vertices, d->n_triangles,
-                           d->square_lights[0], d->spheres, d->n_spheres, &s, &err))
+                           d->square_lights[0], d->spheres, d->n_spheres, &s, &err, ro.build))
         return fail(nullptr, RT_ERR_INVALID_ARG, err);
     info->n_triangles = (uint32_t)s.tri_isect.size();
     info->n_triangle_pairs = (uint32_t)s.pair_isect.size();
@@ -876,13 +945,17 @@ int rt_scene_describe(const rt_scene_desc* d, rt_scene_info* info) {
     const size_t lds = rt::kernel_lds_bytes(info->n_triangles, info->n_triangle_pairs, info->n_spheres,
                                             s.sph_layout_nodes);
     const size_t lds_single = rt::kernel_lds_bytes(info->n_triangles, 0, 0, 0);
-    const bool bvh = info->n_triangles > rt::kTriBvhMinTriangles ||
-                     std::min(lds, lds_single) > rt::kMaxLdsBytes;
+    const bool bvh = info->n_triangles > 0 &&
+                     (ro.mem == rt::SceneMem::kTriBvh ||
+                      (ro.mem == rt::SceneMem::kAuto && (info->n_triangles > rt::kTriBvhMinTriangles ||
+                                                         std::min(lds, lds_single) > rt::kMaxLdsBytes)));
     info->n_triangle_bvh_nodes = bvh ? 2 * info->n_triangles - 1 : 0u;
-    {
-        info->sphere_kernel_lds_bytes =
-            (!s.sph_lds.empty() && lds <= rt::kSphPairLdsMaxBytes) ? (uint32_t)lds : 0u;
-    }
+    // the launcher takes the sphere kernel only for the pair layout (every
+    // triangle paired) and no triangle BVH, with its pair copy within 6 KB
+    info->sphere_kernel_lds_bytes = (!s.sph_lds.empty() && info->n_triangle_pairs > 0 && !bvh &&
+                                     ro.mem == rt::SceneMem::kAuto && lds <= rt::kSphPairLdsMaxBytes)
+                                        ? (uint32_t)lds
+                                        : 0u;
     // box clusters are staged after the pairs in triangle-only scenes
     const size_t lds_clu =
         lds + (info->n_spheres ? 0u : rt::kCluF4 * sizeof(float) * 4 * info->n_box_clusters);

@@ -66,7 +66,8 @@ struct KParams {
     uint32_t samples_total;   // S of `luminance /= samples`
     uint32_t flags;
     uint32_t max_index;       // max Halton index seed+n of this launch (0xFFFFFFFF: unknown/wraps)
-    uint32_t lanes;           // lanes per pixel: 0 = auto, else 1, 4 or 16 (tuning knob)
+    uint32_t lanes;           // lanes per pixel: 0 = auto, else 1, 4 or 16 (rt_create_options)
+    uint32_t walk;            // rt_walk_scheduler: 0 auto, 1 lockstep, 2 free-running lanes
     uint32_t wave_w;          // pixels per wave row (set by the launcher)
     const float4* clusters;   // box clusters, kCluF4 float4 each, or null
     uint32_t nC;              // clusters (0: none)

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <system_error>
 #include <thread>
 
 #include "../../include/rtpt.h"
@@ -276,8 +277,8 @@ struct BvhBuild {
     };
     const SphereGPU* sph;
     float margin;
-    uint32_t leaf_max = 1;  // measured best for config 4 (RTPT_BVH_LEAF sweep 1..8)
-    bool sah = true;        // SAH splits (RTPT_BVH_SAH=0: median of the longest axis)
+    uint32_t leaf_max = 1;  // measured best for config 4 (sphere_leaf_max sweep 1..8)
+    bool sah = true;        // SAH splits (false: median of the longest axis)
     std::vector<uint32_t> ids;
     std::vector<Node> tree;
 
@@ -489,7 +490,7 @@ static void build_sphere_lds(CompiledScene* out) {
 }
 
 static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint32_t n,
-                             float margin) {
+                             float margin, const BuildOptions& opt) {
     out->sph_isect.clear();
     out->sph_perm.clear();
     out->sph_nodes.clear();
@@ -498,11 +499,8 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
     BvhBuild bb;
     bb.sph = spheres;
     bb.margin = margin;
-    if (const char* sm = getenv("RTPT_BVH_SAH")) bb.sah = atoi(sm) != 0;  // tuning knob
-    if (const char* lm = getenv("RTPT_BVH_LEAF")) {  // tuning knob (speed only)
-        const int v = atoi(lm);
-        if (v >= 1 && v <= 255) bb.leaf_max = (uint32_t)v;
-    }
+    bb.sah = opt.sphere_sah;
+    if (opt.sphere_leaf_max >= 1 && opt.sphere_leaf_max <= 255) bb.leaf_max = opt.sphere_leaf_max;
     bb.ids.resize(n);
     for (uint32_t k = 0; k < n; ++k) bb.ids[k] = k;
     bb.build(0, n);
@@ -536,13 +534,12 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
 // a leaf, its first leaf-order triangle | (count - 1) << 24.  Only speed
 // depends on the tree.
 bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<uint32_t>* nodes,
-                   std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm) {
+                   std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm, uint32_t leaf_max,
+                   double trav_cost) {
     const uint32_t n = (uint32_t)tri.size();
     if (n == 0 || n >= (1u << 24)) return false;
-    uint32_t leaf_max = kTriLeafMax;  // tuning knobs (speed only)
-    double trav_cost = 1.0;
-    if (const char* v = getenv("RTPT_TRI_LEAF")) leaf_max = (uint32_t)std::min(128, std::max(1, atoi(v)));
-    if (const char* v = getenv("RTPT_TRI_CT")) trav_cost = atof(v);
+    leaf_max = std::min(128u, std::max(1u, leaf_max));  // speed only
+    if (!(trav_cost > 0.0)) trav_cost = 1.0;
     std::vector<float> bl(3 * (size_t)n), bh(3 * (size_t)n), cen(3 * (size_t)n);
     for (uint32_t k = 0; k < n; ++k) {
         const float* q = tri[k].q;  // v0 0..2, e1 3..5, e2 6..8 (as refit_kernel sees the triangle)
@@ -725,10 +722,20 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
             }
         }
     };
-    {  // the 8 layouts are independent: one host thread each
+    {  // the 8 layouts are independent: one host thread each; a layout whose
+        // thread cannot be started (thread limits) is written on this thread
         std::vector<std::thread> th;
-        for (uint32_t oct = 1; oct < 8; ++oct) th.emplace_back(emit_layout, oct);
+        bool started[8] = {true, false, false, false, false, false, false, false};
+        for (uint32_t oct = 1; oct < 8; ++oct) {
+            try {
+                th.emplace_back(emit_layout, oct);
+                started[oct] = true;
+            } catch (const std::system_error&) {
+            }
+        }
         emit_layout(0);
+        for (uint32_t oct = 1; oct < 8; ++oct)
+            if (!started[oct]) emit_layout(oct);
         for (auto& t : th) t.join();
     }
     sorted->resize(n);
@@ -1040,7 +1047,7 @@ static bool finite3(const rt_float3& v) {
 
 bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float3* verts,
                    uint32_t n_tri, const SquareLightGPU& light, const SphereGPU* spheres,
-                   uint32_t n_sph, CompiledScene* out, const char** err) {
+                   uint32_t n_sph, CompiledScene* out, const char** err, const BuildOptions& opt) {
     if (cam.resolution.x <= 0 || cam.resolution.y <= 0) {
         *err = "camera resolution must be positive";
         return false;
@@ -1125,7 +1132,7 @@ bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float
         }
     }
     out->sph_shade.resize(n_sph);
-    build_sphere_bvh(out, spheres, n_sph, margin);
+    build_sphere_bvh(out, spheres, n_sph, margin, opt);
     for (uint32_t k = 0; k < n_sph; ++k) {
         const SphereGPU& sp = spheres[k];
         const f3 em = from_abi(sp.material.emissive);

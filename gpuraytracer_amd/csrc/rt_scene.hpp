@@ -120,17 +120,28 @@ struct CompiledScene {
     std::vector<MisShade> mis_shade;    // by triangle id
 };
 
-constexpr uint32_t kTriLeafMax = 1;  // triangles per leaf of the host SAH build (RTPT_TRI_LEAF)
+constexpr uint32_t kTriLeafMax = 1;  // triangles per leaf of the host SAH build (default)
 // Host binned-SAH triangle BVH in the compact 8-octant layout (rt_scene.cpp):
 // nodes = 8 layouts x (nodes per layout) entries of 4 words, sorted = records in leaf order,
-// perm = leaf order -> triangle id.  False for n == 0 or n >= 2^24.
+// perm = leaf order -> triangle id.  leaf_max: triangles per leaf at most (1..128),
+// trav_cost: cost of a box step in triangle tests (SAH leaf rule).  False for
+// n == 0 or n >= 2^24.
 bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<uint32_t>* nodes,
-                   std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm);
+                   std::vector<TriIsect>* sorted, std::vector<uint32_t>* perm,
+                   uint32_t leaf_max = kTriLeafMax, double trav_cost = 1.0);
+
+// Speed-only choices of the host builds (rt_create_options, include/rtpt.h):
+// none of them changes a rendered value.
+struct BuildOptions {
+    bool sphere_sah = true;        // exact SAH sweeps (false: median split of the longest axis)
+    uint32_t sphere_leaf_max = 1;  // spheres per leaf (measured best for config 4)
+};
 
 // Validates and precomputes; returns false with *err set on bad input.
 bool compile_scene(const CameraGPU& cam, const MaterialGPU* mats, const rt_float3* verts,
                    uint32_t n_tri, const SquareLightGPU& light, const SphereGPU* spheres,
-                   uint32_t n_sph, CompiledScene* out, const char** err);
+                   uint32_t n_sph, CompiledScene* out, const char** err,
+                   const BuildOptions& opt = BuildOptions());
 
 // ---- scene builders (scene.swift) ------------------------------------------
 struct Material {  // scene.swift:277-282

@@ -13,14 +13,16 @@ reference ``fatalError``s).
 from __future__ import annotations
 
 import ctypes
-from dataclasses import dataclass
+import os
+from dataclasses import dataclass, fields
 
 import numpy as np
 
-from ._native import (RT_COMM_ID_BYTES, RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16,
-                      RT_OUT_NONE, RT_OUT_RGBA8,
-                      CameraGPU, LaunchInfo, MaterialGPU, MisParamsC, RenderParamsC, RtError,
-                      SceneDesc, SceneInfo, SphereGPU, SquareLightGPU, TileLayout, float3, lib)
+from ._native import (LAYOUTS, RT_COMM_ID_BYTES, RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16,
+                      RT_OUT_NONE, RT_OUT_RGBA8, TRI_BUILDS, WALKS,
+                      CameraGPU, CreateOptions, LaunchInfo, MaterialGPU, MisParamsC, RenderParamsC,
+                      RtError, SceneDesc, SceneInfo, SphereGPU, SquareLightGPU, TileLayout, float3,
+                      lib)
 
 DEFAULT_SEED_KEY = 0x5EED00000000
 
@@ -85,6 +87,55 @@ def place_tiles_host(gathered: np.ndarray, width: int, height: int, world: int) 
     _check(lib.rt_place_tiles_host(g.ctypes.data_as(ctypes.c_void_p), width, height, world,
                                    _pixel_flags(fp16, rgba8), frame.ctypes.data_as(ctypes.c_void_p)))
     return frame
+
+
+@dataclass
+class Options:
+    """rt_create_options (include/rtpt.h): per-context, speed-only choices --
+    none changes a rendered value.  Defaults are the library's measured best.
+    ``layout`` in ``LAYOUTS`` (auto, pairs, single, global, pairsmem, sorted,
+    bvh), ``tri_build`` in ``TRI_BUILDS`` (default, host, lbvh, gpusah),
+    ``walk`` in ``WALKS`` (auto, lockstep, free)."""
+
+    layout: str = "auto"
+    lanes: int = 0
+    tri_build: str = "default"
+    tri_leaf_max: int = 0
+    tri_leaf_cost: float = 0.0
+    sphere_leaf_max: int = 0
+    sphere_median: bool = False
+    walk: str = "auto"
+
+    def c(self) -> CreateOptions:
+        o = CreateOptions()
+        o.scene_layout = LAYOUTS[self.layout]
+        o.lanes_per_pixel = self.lanes
+        o.tri_bvh_build = TRI_BUILDS[self.tri_build]
+        o.tri_leaf_max = self.tri_leaf_max
+        o.tri_leaf_cost = self.tri_leaf_cost
+        o.sphere_leaf_max = self.sphere_leaf_max
+        o.sphere_median = 1 if self.sphere_median else 0
+        o.walk_scheduler = WALKS[self.walk]
+        return o
+
+    # tools and the bench take their A/B knobs from the environment; the
+    # library itself reads none (a stray variable cannot change a context)
+    _ENV = {"layout": "RTPT_SCENE_MEM", "lanes": "RTPT_LANES", "tri_build": "RTPT_TRI_BUILD",
+            "tri_leaf_max": "RTPT_TRI_LEAF", "tri_leaf_cost": "RTPT_TRI_CT",
+            "sphere_leaf_max": "RTPT_BVH_LEAF", "walk": "RTPT_WALK"}
+
+    @classmethod
+    def from_env(cls, env=None) -> "Options":
+        """Options from RTPT_* variables (bench.py / tools only)."""
+        env = os.environ if env is None else env
+        o = cls()
+        for f in fields(cls):
+            v = env.get(cls._ENV.get(f.name, ""))
+            if v:
+                setattr(o, f.name, type(getattr(o, f.name))(v) if f.type != "str" else v)
+        if env.get("RTPT_BVH_SAH") == "0":
+            o.sphere_median = True
+        return o
 
 
 class Scene:
@@ -212,10 +263,11 @@ class Scene:
                        ctypes.addressof(base.vertices) + 3 * 34 * 16, 96)
         return cls(base.camera, mats, verts, base.light)
 
-    def describe(self) -> dict:
-        """Device layout rt_create would choose (rt_scene_describe)."""
+    def describe(self, options: Options | None = None) -> dict:
+        """Device layout rt_create would choose (rt_scene_describe_ex)."""
         info = SceneInfo()
-        _check(lib.rt_scene_describe(ctypes.byref(self.desc()), ctypes.byref(info)))
+        opt = None if options is None else ctypes.byref(options.c())
+        _check(lib.rt_scene_describe_ex(ctypes.byref(self.desc()), opt, ctypes.byref(info)))
         return {k: getattr(info, k) for k, _ in SceneInfo._fields_}
 
     def desc(self, device: int = 0) -> SceneDesc:
@@ -290,11 +342,13 @@ class Renderer:
     """renderer.swift's Renderer on the MI355X C-ABI."""
 
     def __init__(self, scene: Scene, device: int = 0, seeds=None,
-                 seed_key: int = DEFAULT_SEED_KEY):
+                 seed_key: int = DEFAULT_SEED_KEY, options: Options | None = None):
         self.scene = scene
         self.device = device
+        self.options = options or Options()
         ctx = ctypes.c_void_p()
-        _check(lib.rt_create(ctypes.byref(scene.desc(device)), ctypes.byref(ctx)))
+        _check(lib.rt_create_ex(ctypes.byref(scene.desc(device)), ctypes.byref(self.options.c()),
+                                ctypes.byref(ctx)))
         self._ctx = ctx
         if seeds is not None:
             s = np.ascontiguousarray(seeds, dtype=np.uint32)

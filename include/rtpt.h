@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RTPT_ABI_VERSION 5
+#define RTPT_ABI_VERSION 6
 
 /* Maximum bounce count: Halton dimensions 2+5b..5+5b must stay inside the
  * 24-entry `primes[]` table (`RTrace/sampling.metal:97-104`); b <= 3. */
@@ -95,8 +95,62 @@ typedef struct rt_render_params {
 } rt_render_params;
 
 /* Renderer.init(): validate and copy the scene to the device, precompute the
- * per-primitive records (edges, normals, shading frames). */
+ * per-primitive records (edges, normals, shading frames).  Default options. */
 int rt_create(const rt_scene_desc* scene, rt_ctx** out_ctx);
+
+/* ---- creation options ----------------------------------------------------
+ * Speed-only choices of one context: which record layout / kernel serves the
+ * scene, how the acceleration structures are built, lanes per pixel.  None of
+ * them changes a rendered value (every layout and build is bit-exact against
+ * the oracle).  They are per context and the library reads no environment
+ * variable: a caller (Swift, C, Python) sets them here or gets the defaults,
+ * which are the measured-best choices.  Zero-initialised fields mean
+ * "default", so `rt_create_options o = {0};` is valid. */
+typedef enum rt_scene_layout {
+    RT_LAYOUT_AUTO = 0,        /* measured best for the scene (box clusters, sphere
+                                  kernel, triangle BVH above 384 triangles)        */
+    RT_LAYOUT_PAIRS = 1,       /* shared-edge pair records in LDS, no box clusters   */
+    RT_LAYOUT_SINGLE = 2,      /* one record per triangle in LDS                     */
+    RT_LAYOUT_GLOBAL = 3,      /* one record per triangle, read from global memory   */
+    RT_LAYOUT_PAIRS_SMEM = 4,  /* pair records by scalar loads, no LDS               */
+    RT_LAYOUT_SORTED = 5,      /* pair records + octant sort of the paths per bounce */
+    RT_LAYOUT_BVH = 6          /* triangle BVH at any triangle count                 */
+} rt_scene_layout;
+
+typedef enum rt_tri_bvh_build {
+    RT_TRI_BVH_DEFAULT = 0,    /* = RT_TRI_BVH_GPU_SAH                               */
+    RT_TRI_BVH_HOST_SAH = 1,   /* host binned SAH (32 bins), uploaded                */
+    RT_TRI_BVH_GPU_LBVH = 2,   /* GPU Morton LBVH (Karras hierarchy + refit)         */
+    RT_TRI_BVH_GPU_SAH = 3     /* GPU binned SAH, the host build's rules             */
+} rt_tri_bvh_build;
+
+typedef enum rt_walk_scheduler {
+    RT_WALK_AUTO = 0,          /* measured best per scene                            */
+    RT_WALK_LOCKSTEP = 1,      /* a wave's lanes run each bounce's queries together  */
+    RT_WALK_FREE = 2           /* every lane runs its own path state; lanes whose
+                                  walk ended park until half the wave has, then
+                                  shade and start their next query together        */
+} rt_walk_scheduler;
+
+typedef struct rt_create_options {
+    uint32_t scene_layout;     /* rt_scene_layout                                    */
+    uint32_t lanes_per_pixel;  /* 0 = auto, else 1, 4 or 16                          */
+    uint32_t tri_bvh_build;    /* rt_tri_bvh_build                                   */
+    uint32_t tri_leaf_max;     /* triangles per BVH leaf at most, 0 = 1; 1..128      */
+    float tri_leaf_cost;       /* SAH leaf rule: box step cost in triangle tests,
+                                  0 = 1.0                                            */
+    uint32_t sphere_leaf_max;  /* spheres per BVH leaf at most, 0 = 1; 1..255        */
+    uint32_t sphere_median;    /* 1: median splits instead of the exact SAH sweep    */
+    uint32_t walk_scheduler;   /* rt_walk_scheduler (BVH scenes)                     */
+    uint32_t reserved[8];      /* must be 0                                          */
+} rt_create_options;
+
+/* The defaults (all zero). */
+void rt_create_options_default(rt_create_options* opt);
+
+/* rt_create with options (NULL = defaults).  RT_ERR_INVALID_ARG for a value
+ * outside its range. */
+int rt_create_ex(const rt_scene_desc* scene, const rt_create_options* opt, rt_ctx** out_ctx);
 
 /* Seed texture (renderer.swift:84-110): W*H uint32 row-major, values are the
  * per-pixel Halton offsets (reference range [0, 2^20)).  W,H must equal the
@@ -268,19 +322,23 @@ int rt_scene_cornell_box_mis(int32_t width, int32_t height, CameraGPU* camera,
                              MaterialGPU* materials, rt_float3* vertices,
                              SquareLightGPU* light, uint32_t* n_triangles);
 
-/* How rt_create would lay a scene out on the device (host-only, no device). */
+/* How rt_create would lay a scene out on the device (host-only, no device),
+ * with default options; rt_scene_describe_ex with `opt` (NULL = defaults). */
 typedef struct rt_scene_info {
     uint32_t n_triangles;
     uint32_t n_triangle_pairs;   /* >0: every (2k,2k+1) shares v0 and an edge -> pair records */
     uint32_t n_spheres;
     uint32_t lds_bytes;          /* intersection records staged per workgroup (0: read from global) */
     uint32_t n_sphere_nodes;     /* sphere BVH nodes per layout (32 B each, 8 layouts, global) */
-    uint32_t n_triangle_bvh_nodes; /* triangle BVH nodes per layout, 2n - 1 at one triangle per leaf (0: LDS layouts) */
+    uint32_t n_triangle_bvh_nodes; /* triangle BVH nodes per layout (0: LDS layouts); 2n - 1 with
+                                      one triangle per leaf (tri_leaf_max <= 1), an upper bound
+                                      with larger leaves */
     uint32_t n_box_clusters;     /* pair runs on the faces of one oriented box (slab-tested first) */
     uint32_t pair_free_mask;     /* pairs in no box cluster (bit k = pair k) */
     uint32_t sphere_kernel_lds_bytes; /* dynamic LDS of the sphere kernel (its pair records; 0: sphere kernel not taken) */
 } rt_scene_info;
 int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
+int rt_scene_describe_ex(const rt_scene_desc* scene, const rt_create_options* opt, rt_scene_info* info);
 
 /* The reference's image epilogue (RTrace/image.swift:35-65): fp16 round trip,
  * ×2 exposure, Reinhard, gamma 1/2.2, clamp, truncating UInt8, alpha 255.

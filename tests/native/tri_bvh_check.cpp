@@ -1,7 +1,7 @@
 // CPU check of the host triangle-BVH build (rt_scene.cpp build_tri_sah), linked
 // against librtpt.so: layout structure, conservative fp16 boxes, and a
 // stackless closest-hit walk of every octant layout equal to brute force.
-//   tri_bvh_check <n> <seed> <dup>   (exit 0 and "ok" on success)
+//   tri_bvh_check <n> <seed> <dup> [leaf_max] [trav_cost]   (exit 0 and "ok" on success)
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -87,6 +87,8 @@ int main(int argc, char** argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 2000;
     const unsigned seed = argc > 2 ? (unsigned)atoi(argv[2]) : 1u;
     const bool dup = argc > 3 && atoi(argv[3]) != 0;
+    const uint32_t leaf_max = argc > 4 ? (uint32_t)atoi(argv[4]) : rt::kTriLeafMax;
+    const double trav_cost = argc > 5 ? atof(argv[5]) : 1.0;
     std::mt19937 g(seed);
     std::uniform_real_distribution<float> U(-2.3f, 2.3f), E(-0.25f, 0.25f);
     std::vector<TriIsect> tri(n);
@@ -101,7 +103,7 @@ int main(int argc, char** argv) {
     const float margin = 1e-4f;
     std::vector<uint32_t> nodes, perm;
     std::vector<TriIsect> sorted;
-    CHECK(rt::build_tri_sah(tri, margin, &nodes, &sorted, &perm), "build failed");
+    CHECK(rt::build_tri_sah(tri, margin, &nodes, &sorted, &perm, leaf_max, trav_cost), "build failed");
     CHECK(nodes.size() % 32 == 0, "node array size %zu", nodes.size());
     const uint32_t total = (uint32_t)(nodes.size() / 32);
     // perm is a permutation, sorted follows it

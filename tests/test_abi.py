@@ -104,6 +104,82 @@ def test_scene_layout_uses_shared_edge_pairs():
     assert big["n_sphere_nodes"] == bvh_nodes(5000)
 
 
+def test_create_options_are_validated_without_a_device():
+    """rt_create_ex checks rt_create_options before it looks for a device:
+    out-of-range values come back as RT_ERR_INVALID_ARG with a message."""
+    ctx = ctypes.c_void_p()
+    desc = g.Scene.cornell_box(8, 8).desc()
+    o = _native.CreateOptions()
+    g.lib.rt_create_options_default(ctypes.byref(o))
+    assert bytes(o) == bytes(ctypes.sizeof(o))  # the defaults are all zero
+    for field, bad in [("scene_layout", 7), ("lanes_per_pixel", 2), ("tri_bvh_build", 9),
+                       ("tri_leaf_max", 129), ("sphere_leaf_max", 256), ("sphere_median", 2),
+                       ("walk_scheduler", 3), ("tri_leaf_cost", -1.0)]:
+        q = _native.CreateOptions()
+        setattr(q, field, bad)
+        assert g.lib.rt_create_ex(ctypes.byref(desc), ctypes.byref(q), ctypes.byref(ctx)) == 1, field
+        assert field.encode() in g.lib.rt_last_error(None), field
+        assert not ctx.value
+    q = _native.CreateOptions()
+    q.reserved[3] = 1
+    assert g.lib.rt_create_ex(ctypes.byref(desc), ctypes.byref(q), ctypes.byref(ctx)) == 1
+    assert b"reserved" in g.lib.rt_last_error(None)
+
+
+def test_library_reads_no_environment():
+    """Kernel-selecting knobs are rt_create_options fields: no object file of
+    librtpt.so that is built from this repository's sources imports getenv.
+    (rocPRIM's device sort in rt_lbvh.o reads ROCPRIM_USE_ATOMIC_BLOCK_ID, a
+    switch of that third-party library's own block ordering.)"""
+    import glob
+    import subprocess
+    objs = sorted(glob.glob(os.path.join(ROOT, "build", "*.o")))
+    if not objs:
+        pytest.skip("no build/ objects")
+    users = []
+    for o in objs:
+        und = subprocess.run(["nm", "--undefined-only", o], capture_output=True, text=True).stdout
+        if "getenv" in und:
+            users.append(os.path.basename(o))
+    assert users in ([], ["rt_lbvh.o"]), users
+    src = "".join(open(f).read() for f in glob.glob(os.path.join(ROOT, "gpuraytracer_amd", "csrc", "*")))
+    assert "getenv" not in src
+
+
+def test_describe_follows_options_and_the_launcher():
+    cornell = g.Scene.cornell_box(64, 48)
+    forced = cornell.describe(g.Options(layout="bvh"))
+    assert forced["n_triangle_bvh_nodes"] == 2 * 36 - 1 and forced["lds_bytes"] == 0
+    # spheres with triangles that cannot be paired: the launcher takes the
+    # single-record layout and the 32-B-node walks, not the one-wave sphere kernel
+    sph = g.Scene.random_spheres(32, 16, 100)
+    n = 11  # the 12 room/light triangles minus one: odd, no pair layout
+    mats = (g.MaterialGPU * n)()
+    verts = (g.float3 * (3 * n))()
+    ctypes.memmove(ctypes.addressof(mats), ctypes.addressof(sph.materials), n * 48)
+    ctypes.memmove(ctypes.addressof(verts), ctypes.addressof(sph.vertices), 3 * n * 16)
+    odd = g.Scene(sph.camera, mats, verts, sph.light, sph.spheres)
+    info = odd.describe()
+    assert info["n_triangle_pairs"] == 0 and info["sphere_kernel_lds_bytes"] == 0
+    assert sph.describe()["sphere_kernel_lds_bytes"] == 6 * 112
+    # a forced layout also leaves the sphere kernel
+    assert sph.describe(g.Options(layout="pairs"))["sphere_kernel_lds_bytes"] == 0
+
+
+def test_options_from_env_is_explicit():
+    """The RTPT_* variables reach a context only through Options.from_env()
+    (bench.py and tools/); Renderer's default is the library's defaults."""
+    env = {"RTPT_SCENE_MEM": "sorted", "RTPT_LANES": "16", "RTPT_TRI_BUILD": "lbvh",
+           "RTPT_TRI_LEAF": "4", "RTPT_TRI_CT": "2.5", "RTPT_BVH_LEAF": "3", "RTPT_BVH_SAH": "0",
+           "RTPT_WALK": "free"}
+    o = g.Options.from_env(env)
+    assert (o.layout, o.lanes, o.tri_build, o.tri_leaf_max, o.tri_leaf_cost, o.sphere_leaf_max,
+            o.sphere_median, o.walk) == ("sorted", 16, "lbvh", 4, 2.5, 3, True, "free")
+    c = o.c()
+    assert (c.scene_layout, c.lanes_per_pixel, c.tri_bvh_build, c.walk_scheduler) == (5, 16, 2, 2)
+    assert g.Options.from_env({}) == g.Options()
+
+
 def _with_quads(base, n_quads, seed=3):
     """base's triangles + n_quads random planar quads (one shared-edge pair each)."""
     import ctypes

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from gpuraytracer_amd import RenderParams, Renderer, Scene, seed_splitmix
+from gpuraytracer_amd import Options, RenderParams, Renderer, Scene, seed_splitmix
 from test_gpu_parity import assert_parity
 
 pytestmark = pytest.mark.gpu
@@ -46,15 +46,14 @@ def test_headline_instantiation_full_frame_32spp_vs_oracle():
 
 
 @pytest.mark.parametrize("rows", [(0, 3), (361, 4), (539, 2), (1076, 4)])
-def test_headline_instantiation_256spp_row_bands_vs_oracle(rows, monkeypatch):
+def test_headline_instantiation_256spp_row_bands_vs_oracle(rows):
     """Full-width 1080p bands at the bench's 256 spp with 4 lanes per pixel
     forced (a small launch alone would pick 16): 64 rounds per lane, tables
     on, the same instantiation as the timed whole-frame launch."""
-    monkeypatch.setenv("RTPT_LANES", "4")
     start, count = rows
     s = Scene.cornell_box(1920, 1080)
     sd = seed_splitmix(1920, 1080)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(lanes=4)) as r:
         out = r.render(RenderParams(spp=256, bounces=3, row_start=start, row_count=count))
         _timed(r)
     ref = oracle_lib.render(s, sd, 256, 3, row_start=start, row_count=count, threads=16)
@@ -63,18 +62,17 @@ def test_headline_instantiation_256spp_row_bands_vs_oracle(rows, monkeypatch):
 
 @pytest.mark.parametrize("lanes,spp", [(4, 32), (16, 128)])
 @pytest.mark.parametrize("top", [3 ** 13 - 1, 3 ** 13])
-def test_halton_index_bound_edges_with_tables(top, lanes, spp, monkeypatch):
+def test_halton_index_bound_edges_with_tables(top, lanes, spp):
     """The fixed-digit boundary (largest index 3^13 - 1: the table kernel with
     halton_tab's continuation T_D[i mod b^k] + digits of i / b^k, at >= 8
     rounds per lane with L = 4 and L = 16; 3^13: the generic loop)."""
-    monkeypatch.setenv("RTPT_LANES", str(lanes))
     W, H = 40, 24
     rng = np.random.default_rng(top + lanes)
     sd = rng.integers(top - spp + 1 - 400000, top - spp + 2, (H, W), dtype=np.int64)
     sd[5, 9] = top - spp + 1  # max index = top
     sd = sd.astype(np.uint32)
     s = Scene.cornell_box(W, H)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(lanes=lanes)) as r:
         out = r.render(RenderParams(spp=spp, bounces=3))
         info = r.last_launch()
     small = top < 3 ** 13

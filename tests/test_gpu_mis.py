@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from gpuraytracer_amd import (CameraGPU, MaterialGPU, MisParams, Renderer, RtError, Scene,
+from gpuraytracer_amd import (CameraGPU, MaterialGPU, MisParams, Options, Renderer, RtError, Scene,
                               SquareLightGPU, float3)
 
 pytestmark = pytest.mark.gpu
@@ -95,14 +95,27 @@ def test_mis_device_outputs_match_host():
 
 
 @pytest.mark.parametrize("layout", ["single", "smem", "pairs"])
-def test_mis_scene_layouts_bit_exact(layout, monkeypatch):
-    monkeypatch.setenv("RTPT_SCENE_MEM", layout)
+def test_mis_scene_layouts_bit_exact(layout):
     s = Scene.cornell_box_mis(40, 24)
-    with Renderer(s) as r:
+    with Renderer(s, options=Options(layout=layout)) as r:
         out, out8 = r.render_mis(MisParams(camera_rays=2, mis_samples=12))
     ref, ref8 = oracle_lib.render_mis(s, 2, 12)
     assert_same(out, ref, layout)
     assert_same(out8, ref8, layout)
+
+
+def test_mis_lds_layout_above_64k_with_the_stash_bit_exact():
+    """A forced single-record LDS layout whose records (96 B per triangle:
+    intersection + shading) take 57.6 KB: with the 15 KB stash on top the
+    workgroup asks for 72.6 KB of dynamic LDS (hipFuncSetAttribute above
+    64 KB, rt_mis.hip launch_mis_g) instead of falling back to global memory."""
+    s = Scene.random_triangles(40, 24, 564, seed=3)  # 600 triangles
+    assert 49 * 1024 < 96 * 600 <= 64 * 1024
+    with Renderer(s, options=Options(layout="single")) as r:
+        out, out8 = r.render_mis(MisParams(camera_rays=2, mis_samples=9))
+    ref, ref8 = oracle_lib.render_mis(s, 2, 9)
+    assert_same(out, ref, "single 600")
+    assert_same(out8, ref8, "single 600")
 
 
 def test_mis_box_clusters_rotated_boxes_bit_exact():

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from gpuraytracer_amd import (CameraGPU, MaterialGPU, RenderParams, Renderer, RtError, Scene,
+from gpuraytracer_amd import (CameraGPU, MaterialGPU, Options, RenderParams, Renderer, RtError, Scene,
                               SphereGPU, SquareLightGPU, float3, seed_splitmix)
 
 pytestmark = pytest.mark.gpu
@@ -98,12 +98,11 @@ def test_spheres_1000_vs_oracle():
 
 
 @pytest.mark.parametrize("leaf", ["2", "3", "8"])
-def test_sphere_bvh_multi_sphere_leaves(leaf, monkeypatch):
-    # RTPT_BVH_LEAF > 1: leaves hold several spheres (the default is one per leaf)
-    monkeypatch.setenv("RTPT_BVH_LEAF", leaf)
+def test_sphere_bvh_multi_sphere_leaves(leaf):
+    # sphere_leaf_max > 1: leaves hold several spheres (the default is one per leaf)
     s = Scene.random_spheres(40, 24, 700, seed=5)
     sd = seed_splitmix(40, 24)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(sphere_leaf_max=int(leaf))) as r:
         out = r.render(RenderParams(spp=2, bounces=3))
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), "leaf" + leaf)
 
@@ -124,15 +123,13 @@ def test_duplicate_spheres_tie_to_lower_id():
 
 
 @pytest.mark.parametrize("layout", ["auto", "pairs"])
-def test_sphere_bvh_lds_and_global_walks_bit_exact(layout, monkeypatch):
+def test_sphere_bvh_lds_and_global_walks_bit_exact(layout):
     """auto: the compact fp16 sphere BVH (8 octant layouts, near/far boxes,
     per-lane walks); pairs: the 32-B-node BVH read with scalar loads in the
     pair-record kernel.  Both are the oracle."""
-    if layout != "auto":
-        monkeypatch.setenv("RTPT_SCENE_MEM", layout)
     s = Scene.random_spheres(40, 24, 700, seed=13)
     sd = seed_splitmix(40, 24, key=13)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(layout=layout)) as r:
         out = r.render(RenderParams(spp=3, bounces=3))
     assert_parity(out, oracle_lib.render(s, sd, 3, 3), f"spheres700-{layout}")
 
@@ -296,14 +293,13 @@ def test_errors_are_status_codes():
 
 
 @pytest.mark.parametrize("layout", ["single", "smem", "sorted", "pairsmem", "bvh", "pairs"])
-def test_alternate_scene_layouts_bit_exact(layout, monkeypatch):
+def test_alternate_scene_layouts_bit_exact(layout):
     """The single-triangle LDS layout, the global (scalar-load) layout and the
     octant-sorted path kernel give the same bits as the default pair kernel
     and the oracle."""
-    monkeypatch.setenv("RTPT_SCENE_MEM", layout)
     s = Scene.cornell_box(56, 40)
     sd = seed_splitmix(56, 40, key=99)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(layout=layout)) as r:
         out = r.render(RenderParams(spp=3, bounces=3))
     assert_parity(out, oracle_lib.render(s, sd, 3, 3), layout)
 
@@ -424,31 +420,38 @@ def ctypes_memmove(dst, src, n):
     ctypes.memmove(ctypes.addressof(dst), ctypes.addressof(src), n)
 
 
-@pytest.mark.parametrize("build", ["sah", "lbvh"])
+TRI_BUILD_OPTIONS = {
+    "host": Options(tri_build="host"),
+    "lbvh": Options(tri_build="lbvh"),
+    # leaves of up to 4 triangles (word first | (count - 1) << 24): the count > 1
+    # loops of tri_leaf_closest / tri_leaf_any in the packet and parked-leaf walks
+    "host_leaf4": Options(tri_build="host", tri_leaf_max=4, tri_leaf_cost=2.0),
+}
+
+
+@pytest.mark.parametrize("build", list(TRI_BUILD_OPTIONS))
 @pytest.mark.parametrize("n,dup", [(3000, False), (2500, True)])
-def test_triangle_bvh_gpu_build_bit_exact(n, dup, build, monkeypatch):
-    """Both triangle-BVH builds: the host binned-SAH tree (default) and the
-    GPU Morton LBVH (RTPT_TRI_BUILD=lbvh, rt_lbvh.hip), same compact layout."""
-    if build == "lbvh":
-        monkeypatch.setenv("RTPT_TRI_BUILD", "lbvh")
+def test_triangle_bvh_gpu_build_bit_exact(n, dup, build):
+    """Every triangle-BVH build -- the host binned-SAH tree, the GPU Morton
+    LBVH (rt_lbvh.hip), the GPU binned SAH (rt_gsah.hip) and multi-triangle
+    leaves -- in the same compact layout, against the oracle."""
     s = triangle_soup(40, 24, n, seed=n, dup=dup)
     assert s.describe()["lds_bytes"] == 0  # does not fit LDS: the BVH path
     sd = seed_splitmix(40, 24)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=TRI_BUILD_OPTIONS[build]) as r:
         out = r.render(RenderParams(spp=2, bounces=3))
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"soup{n}")
 
 
 def test_triangle_bvh_forced_on_cornell_and_mis(monkeypatch):
-    monkeypatch.setenv("RTPT_SCENE_MEM", "bvh")
     s = Scene.cornell_box(64, 48)
     sd = seed_splitmix(64, 48)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(layout="bvh")) as r:
         out = r.render(RenderParams(spp=3, bounces=4))
     assert_parity(out, oracle_lib.render(s, sd, 3, 4), "bvh cornell")
     from gpuraytracer_amd import MisParams
     m = Scene.cornell_box_mis(40, 24)
-    with Renderer(m) as r:
+    with Renderer(m, options=Options(layout="bvh")) as r:
         got, got8 = r.render_mis(MisParams(camera_rays=2, mis_samples=12))
     ref, ref8 = oracle_lib.render_mis(m, 2, 12)
     assert_parity(got, ref, "bvh mis")
@@ -456,14 +459,12 @@ def test_triangle_bvh_forced_on_cornell_and_mis(monkeypatch):
 
 
 @pytest.mark.parametrize("lanes", ["1", "4", "16", "auto"])
-def test_lanes_per_pixel_and_interleaved_rows_bit_exact(lanes, monkeypatch):
+def test_lanes_per_pixel_and_interleaved_rows_bit_exact(lanes):
     # 1, 4 or 16 lanes per pixel (samples shuffled back into sample order) and
     # one-row wave tiles for interleaved rows all give the oracle's sums
-    if lanes != "auto":
-        monkeypatch.setenv("RTPT_LANES", lanes)
     s = Scene.cornell_box(56, 40)
     sd = seed_splitmix(56, 40)
-    with Renderer(s, seeds=sd) as r:
+    with Renderer(s, seeds=sd, options=Options(lanes=0 if lanes == "auto" else int(lanes))) as r:
         full = r.render(RenderParams(spp=19, bounces=3))
         tile = r.render(RenderParams(spp=19, bounces=3, row_start=2, row_step=5))
     ref = oracle_lib.render(s, sd, 19, 3)
@@ -472,7 +473,7 @@ def test_lanes_per_pixel_and_interleaved_rows_bit_exact(lanes, monkeypatch):
 
 
 @pytest.mark.parametrize("mem", [None, "bvh", "spheres"])
-def test_zero_light_terms_black_materials_bit_exact(mem, monkeypatch):
+def test_zero_light_terms_black_materials_bit_exact(mem):
     """Lanes whose light term is exactly 0 skip their shadow query (DESIGN.md
     §3.14): black boxes and a black wall make whole paths carry a zero
     throughput (every later light term is 0), and the ceiling and the light's
@@ -489,11 +490,9 @@ def test_zero_light_terms_black_materials_bit_exact(mem, monkeypatch):
         for k in range(0, 300, 2):
             m = sph[k].material
             m.diffuse.x = m.diffuse.y = m.diffuse.z = 0.0
-    elif mem == "bvh":
-        monkeypatch.setenv("RTPT_SCENE_MEM", "bvh")
     scene = Scene(s.camera, mats, s.vertices, s.light, sph)
     sd = seed_splitmix(48, 32, key=9)
-    with Renderer(scene, seeds=sd) as r:
+    with Renderer(scene, seeds=sd, options=Options(layout="bvh" if mem == "bvh" else "auto")) as r:
         out = r.render(RenderParams(spp=4, bounces=3))
     assert_parity(out, oracle_lib.render(scene, sd, 4, 3), f"black materials {mem}")
     assert np.isfinite(out).all()

@@ -31,11 +31,6 @@ def checker(tmp_path_factory):
 
 @pytest.mark.parametrize("n,seed,dup,leaf", [(3000, 1, 0, None), (2500, 2, 1, None), (3000, 3, 0, "4")])
 def test_host_sah_triangle_bvh_layout_and_walks(checker, n, seed, dup, leaf):
-    env = dict(os.environ)
-    env.pop("RTPT_TRI_LEAF", None)
-    if leaf:
-        env["RTPT_TRI_LEAF"] = leaf
-        env["RTPT_TRI_CT"] = "2"
-    r = subprocess.run([checker, str(n), str(seed), str(dup)], capture_output=True, text=True,
-                       env=env, timeout=300)
+    args = [checker, str(n), str(seed), str(dup)] + ([leaf, "2"] if leaf else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr

@@ -70,11 +70,11 @@ def main():
     a = ap.parse_args()
 
     import torch
-    from gpuraytracer_amd import MisParams, Renderer, Scene
+    from gpuraytracer_amd import MisParams, Options, Renderer, Scene
 
     torch.cuda.set_device(0)
     scene = Scene.cornell_box_mis(a.width, a.height)
-    r = Renderer(scene)
+    r = Renderer(scene, options=Options.from_env())
     out = torch.empty((a.height, a.width, 4), dtype=torch.float32, device="cuda")
     out8 = torch.empty((a.height, a.width, 4), dtype=torch.uint8, device="cuda")
     p = MisParams(camera_rays=a.camera_rays, mis_samples=a.mis_samples)

@@ -52,7 +52,7 @@ def main(argv=None):
     ap.add_argument("--quads", default="0,36,37", help="extra planar quads per case")
     a = ap.parse_args(argv)
     import gpuraytracer_amd as g
-    from gpuraytracer_amd import Renderer, RenderParams, Scene, seed_splitmix
+    from gpuraytracer_amd import Options, Renderer, RenderParams, Scene, seed_splitmix
     base = Scene.cornell_box(a.width, a.height)
     sph = Scene.random_spheres(a.width, a.height, a.spheres, seed=42).spheres
     sd = seed_splitmix(a.width, a.height, key=42)
@@ -62,7 +62,7 @@ def main(argv=None):
             s = Scene(base.camera, mats, verts, base.light, sph)
         else:
             s = Scene(base.camera, base.materials, base.vertices, base.light, sph)
-        with Renderer(s, seeds=sd) as r:
+        with Renderer(s, seeds=sd, options=Options.from_env()) as r:
             p = RenderParams(spp=a.spp, bounces=3)
             r.render(p)  # warm-up
             ms = []

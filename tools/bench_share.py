@@ -7,12 +7,12 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401  (one HIP runtime)
-from gpuraytracer_amd import RenderParams, Renderer, Scene  # noqa: E402
+from gpuraytracer_amd import RenderParams, Options, Renderer, Scene  # noqa: E402
 from gpuraytracer_amd.tiles import rank_rows  # noqa: E402
 
 W, H, SPP = 1920, 1080, 256
 res = {}
-with Renderer(Scene.cornell_box(W, H)) as r:
+with Renderer(Scene.cornell_box(W, H), options=Options.from_env()) as r:
     for n in (1, 2, 4, 8):
         start, step, rows = rank_rows(H, n, 0)
         p = RenderParams(spp=SPP * n, bounces=3, row_start=start, row_step=step, row_count=rows)

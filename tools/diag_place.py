@@ -3,12 +3,12 @@ import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 import numpy as np, torch
-from gpuraytracer_amd import RenderParams, Renderer, Scene
+from gpuraytracer_amd import RenderParams, Options, Renderer, Scene
 from test_gpu_gather import _render_tiles
 mode = sys.argv[1]
 W, H = 1920, 1080
 s = Scene.cornell_box(W, H)
-with Renderer(s) as r:
+with Renderer(s, options=Options.from_env()) as r:
     st = torch.cuda.current_stream()
     print("stream handle", st.cuda_stream)
     ref = r.render(RenderParams(spp=2))

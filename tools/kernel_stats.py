@@ -10,10 +10,10 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: F401,E402  (one HIP runtime)
-from gpuraytracer_amd import RenderParams, Renderer, Scene, lib  # noqa: E402
+from gpuraytracer_amd import RenderParams, Options, Renderer, Scene, lib  # noqa: E402
 
 W, H, SPP = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-with Renderer(Scene.cornell_box(W, H)) as r:
+with Renderer(Scene.cornell_box(W, H), options=Options.from_env()) as r:
     r.render(RenderParams(spp=SPP, bounces=3))
     info = r.last_launch()
     st = (ctypes.c_uint64 * 32)()

@@ -6,7 +6,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401  (one HIP runtime)
-from gpuraytracer_amd import RenderParams, Renderer, Scene  # noqa: E402
+from gpuraytracer_amd import RenderParams, Options, Renderer, Scene  # noqa: E402
 
 CASES = [  # (W, H, row_step, spp)
     (1920, 1080, 1, 256), (1920, 1080, 2, 512), (1920, 1080, 8, 2048),
@@ -15,7 +15,7 @@ CASES = [  # (W, H, row_step, spp)
 for lanes in ("4", "16"):
     os.environ["RTPT_LANES"] = lanes
     for W, H, n, spp in CASES:
-        with Renderer(Scene.cornell_box(W, H)) as r:
+        with Renderer(Scene.cornell_box(W, H), options=Options.from_env()) as r:
             p = RenderParams(spp=spp, row_start=0, row_step=n, row_count=(H + n - 1) // n)
             r.render(p)
             ms = []

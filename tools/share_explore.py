@@ -8,7 +8,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401  (one HIP runtime)
-from gpuraytracer_amd import RenderParams, Renderer, Scene  # noqa: E402
+from gpuraytracer_amd import RenderParams, Options, Renderer, Scene  # noqa: E402
 
 W, H, SPP = 1920, 1080, 256
 res = {}
@@ -26,7 +26,7 @@ def t(r, p, rows):
 
 for lanes in ("4", "16"):
     os.environ["RTPT_LANES"] = lanes
-    with Renderer(Scene.cornell_box(W, H)) as r:
+    with Renderer(Scene.cornell_box(W, H), options=Options.from_env()) as r:
         res[f"full_L{lanes}"] = t(r, RenderParams(spp=SPP), H)
         for k in (0, 4):
             res[f"interleaved8_rank{k}_L{lanes}"] = t(

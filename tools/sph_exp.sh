@@ -1,6 +1,6 @@
 #!/bin/bash
 # Config-4 walk experiments on the GPU box: timing of abvar variants under
-# environment settings, then RT_STATS counters of both sphere walks.
+# environment settings (Options.from_env), then RT_STATS counters of the sphere walks.
 #   tools/sph_exp.sh <tag> <variant:ENV=VAL,...>...
 set -u
 TAG=$1; shift
@@ -10,10 +10,8 @@ for spec in "$@"; do
   v=${spec%%:*}; envs=${spec#*:}; [ "$envs" = "$spec" ] && envs=""
   bash tools/ab_env_bench.sh "$TAG" "$v" ${envs//,/ } || exit 1
 done
-if [ -f abvar/librtpt_stats.so ]; then
-  for w in binary wide; do
-    RTPT_LIB=$R/abvar/librtpt_stats.so RTPT_SPH_WALK=$w timeout -k 10 120 python tools/sphere_stats.py 480 270 16 \
-      > "$OUT/stats_$w.json" 2> "$OUT/stats_$w.err" || { tail -5 "$OUT/stats_$w.err" >&2; exit 1; }
-    echo "stats $w: $(python3 -c "import json;d=json.load(open('$OUT/stats_$w.json'));print({k:{q:round(x,2) for q,x in v.items() if q in ('steps_per_walk','step_lane_util','lane_steps_per_lane_walk','walks_per_sample')} for k,v in d.items() if k!='packet'})")" >&2
-  done
+if [ -f abvar/librtpt_stats.so ]; then  # one RT_STATS pass of the sphere walks
+  RTPT_LIB=$R/abvar/librtpt_stats.so timeout -k 10 120 python tools/sphere_stats.py 480 270 16 \
+    > "$OUT/stats.json" 2> "$OUT/stats.err" || { tail -5 "$OUT/stats.err" >&2; exit 1; }
+  echo "stats: $(python3 -c "import json;d=json.load(open('$OUT/stats.json'));print({k:{q:round(x,2) for q,x in v.items() if q in ('steps_per_walk','step_lane_util','lane_steps_per_lane_walk','walks_per_sample')} for k,v in d.items() if k!='packet'})")" >&2
 fi

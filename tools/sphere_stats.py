@@ -8,12 +8,12 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: F401,E402  (one HIP runtime)
-from gpuraytracer_amd import RenderParams, Renderer, Scene, lib  # noqa: E402
+from gpuraytracer_amd import RenderParams, Options, Renderer, Scene, lib  # noqa: E402
 
 a = sys.argv[1:]
 W, H, SPP = (int(a[0]), int(a[1]), int(a[2])) if len(a) >= 3 else (480, 270, 16)
 NS = int(a[3]) if len(a) >= 4 else 1000
-with Renderer(Scene.random_spheres(W, H, NS, seed=42)) as r:
+with Renderer(Scene.random_spheres(W, H, NS, seed=42), options=Options.from_env()) as r:
     r.render(RenderParams(spp=SPP, bounces=3))
     st = (ctypes.c_uint64 * 32)()
     assert lib.rt_debug_stats(r._ctx, st, 32) == 0, lib.rt_last_error(r._ctx)
