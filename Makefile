@@ -48,8 +48,42 @@ $(PKG)/rtrace: $(SRC)/rtrace_main.cpp $(PKG)/librtpt.so $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
+# ---- sanitizer build of the CPU code (ASan/UBSan) -------------------
+# build_asan/liboracle.so  the oracle, -fsanitize=address,undefined
+# build_asan/librtpt.so    the host C++ of the library (scene compile, host BVH
+#                          builds on host threads, tile layout/placement, image
+#                          epilogue, C-ABI argument handling) sanitized, linked
+#                          with the device objects of build/
+# `make asan-test` runs the CPU tests of that code (tests/run_sanitized.py)
+# under it; UBSan findings abort (-fno-sanitize-recover).
+ASAN := build_asan
+SAN := -fsanitize=address,undefined -fno-sanitize-recover=all -fno-omit-frame-pointer -g -shared-libasan
+ASAN_RT := $(shell $(HOSTCXX) -print-file-name=libclang_rt.asan-x86_64.so)
+ASAN_HOST := $(ASAN)/rt_api.o $(ASAN)/rt_scene.o $(ASAN)/rt_image.o
+
+$(ASAN):
+	mkdir -p $(ASAN)
+
+$(ASAN)/rt_api.o: $(SRC)/rt_api.cpp $(ALLSRC) | $(ASAN)
+	$(HOSTCXX) $(HOSTFLAGS) $(SAN) -DRT_SRC_SHA='"$(SRC_SHA)"' -c $< -o $@
+
+$(ASAN)/%.o: $(SRC)/%.cpp $(HDRS) | $(ASAN)
+	$(HOSTCXX) $(HOSTFLAGS) $(SAN) -c $< -o $@
+
+$(ASAN)/librtpt.so: $(ASAN_HOST) $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o
+	$(HOSTCXX) -shared $(SAN) -o $@ $^ -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
+
+$(ASAN)/liboracle.so: oracle/pt_oracle.c oracle/pt_oracle.h include/rt_types.h | $(ASAN)
+	$(HOSTCXX:clang++=clang) -x c -std=c11 -O1 -mfma -ffp-contract=off -fno-fast-math -fPIC -Wall -pthread \
+	    $(SAN) -shared -o $@ oracle/pt_oracle.c -lm
+
+asan: $(ASAN)/librtpt.so $(ASAN)/liboracle.so
+
+asan-test: asan
+	RTPT_SAN_DIR=$(abspath $(ASAN)) RTPT_SAN_RT=$(ASAN_RT) python3 tests/run_sanitized.py
+
 clean:
-	rm -rf $(BLD) $(PKG)/librtpt.so $(PKG)/rtrace
+	rm -rf $(BLD) $(ASAN) $(PKG)/librtpt.so $(PKG)/rtrace
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib oracle clean
+.PHONY: all lib oracle clean asan asan-test

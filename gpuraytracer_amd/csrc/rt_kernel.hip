@@ -604,6 +604,8 @@ void path_trace_kernel(KParams P) {
     }
 }
 
+#include "rt_free.hpp"
+
 template <int B, bool SPH, bool SMALL>
 __global__ __launch_bounds__(kBlockThreads, kMinWavesPerEu) void path_trace_sorted_kernel(
     KParams P) {
@@ -746,6 +748,8 @@ inline int lanes_per_pixel(const KParams& P, int geo) {
 }
 
 constexpr int kGeoPairSorted = 3;  // pair records + per-bounce octant sort of the paths
+constexpr int kGeoFreeSph = 8;     // free-running lanes, sphere scene (rt_free.hpp)
+constexpr int kGeoFreeTri = 9;     // free-running lanes, triangle BVH
 
 // The most recent launch of this thread (launch_path_trace copies it out).
 thread_local LaunchInfo g_last;
@@ -837,8 +841,34 @@ hipError_t launch_sorted_t(const KParams& P, size_t lds_bytes, hipStream_t strea
     return hipGetLastError();
 }
 
+// The free-running kernel (rt_free.hpp): one pixel per lane, 8x8-pixel waves
+// (one row of 64 pixels for interleaved rows), one-wave workgroups.
+template <int B, int GEO, bool SMALL>
+hipError_t launch_free_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
+    KParams Q = P;
+    Q.wave_w = (P.row_step > 1) ? 64u : 8u;
+    const uint32_t TY = 64u / Q.wave_w;
+    const dim3 grid((P.W + Q.wave_w - 1) / Q.wave_w, (P.row_count + TY - 1) / TY);
+    const size_t lds = GEO == kGeoSphLds ? lds_bytes : 0;
+    note_launch<B, GEO, GEO == kGeoSphLds, SMALL, 1>("path_free_kernel", Q, grid, kFreeThreads, lds);
+    hipLaunchKernelGGL((path_free_kernel<B, GEO, SMALL>), grid, dim3(kFreeThreads), lds, stream, Q);
+    return hipGetLastError();
+}
+
+template <int B, int GEO>
+hipError_t launch_free(const KParams& P, size_t lds_bytes, hipStream_t stream) {
+    if constexpr (B < 1) {
+        return hipErrorInvalidValue;
+    } else {
+        return P.max_index < kSmallIndexMax ? launch_free_t<B, GEO, true>(P, lds_bytes, stream)
+                                            : launch_free_t<B, GEO, false>(P, lds_bytes, stream);
+    }
+}
+
 template <int B>
 hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t stream) {
+    if (geo == kGeoFreeSph) return launch_free<B, kGeoSphLds>(P, lds_bytes, stream);
+    if (geo == kGeoFreeTri) return launch_free<B, kGeoTriBvh>(P, lds_bytes, stream);
     if (geo == kGeoPairSorted) {
         const bool small = P.max_index < kSmallIndexMax;
         const size_t bytes = lds_bytes + sorted_lds_extra_bytes();
@@ -898,8 +928,15 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     if (geo == kGeoPairLds && mem == SceneMem::kPairSorted &&
         lds_bytes + sorted_lds_extra_bytes() <= kMaxLdsBytes)
         geo = kGeoPairSorted;
+    // the free-running kernel for BVH scenes (rt_create_options.walk_scheduler)
+    if (bounces >= 1 && P.walk == kWalkFree) {
+        if (geo == kGeoSphLds) geo = kGeoFreeSph;
+        if (geo == kGeoTriBvh && P.nS == 0) geo = kGeoFreeTri;
+    }
 #ifdef RT_DEV_ISA  // ISA-inspection builds only (tools/isa.sh): the two headline layouts at B = 3
     if (bounces != 3) return hipErrorInvalidValue;
+    if (geo == kGeoFreeSph) return launch_free<3, kGeoSphLds>(P, lds_total, stream);
+    if (geo == kGeoFreeTri) return launch_free<3, kGeoTriBvh>(P, lds_total, stream);
     return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_total, stream)
                               : launch_g<3, kGeoSphLds>(P, lds_total, stream);
 #endif

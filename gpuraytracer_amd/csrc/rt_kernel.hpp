@@ -81,6 +81,8 @@ struct LaunchInfo {
     uint32_t lanes, tables, small, threads, grid_x, grid_y, lds;
 };
 // Where the workgroup reads the intersection records from.
+// rt_walk_scheduler (include/rtpt.h)
+constexpr uint32_t kWalkAuto = 0, kWalkLockstep = 1, kWalkFree = 2;
 enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5, kPairLds = 6 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream,
                              LaunchInfo* info);

@@ -21,6 +21,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) — run with -m gpu")
 
 
+def native_toolchain(cxx):
+    """(compiler, extra flags, librtpt directory) for the tests' small C++
+    checkers: the plain build, or under tests/run_sanitized.py (RTPT_SAN_DIR)
+    clang++ with ASan/UBSan linked against the sanitizer build (make asan)."""
+    san_dir = os.environ.get("RTPT_SAN_DIR")
+    if not san_dir:
+        return cxx, [], os.path.join(ROOT, "gpuraytracer_amd")
+    flags = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+             "-g", "-shared-libasan"]
+    return "/opt/rocm/llvm/bin/clang++", flags, san_dir
+
+
 def _lib_is_fresh(path):
     """Whether the built librtpt.so carries this tree's source hash (its
     rt_build_sha() string), read from the file's bytes: loading it here would

@@ -7,7 +7,8 @@ import numpy as np
 from gpuraytracer_amd import CameraGPU, MaterialGPU, SphereGPU, SquareLightGPU, float3
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-_lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+# RTPT_ORACLE_LIB: the sanitizer build (make asan-test, tests/run_sanitized.py)
+_lib = ctypes.CDLL(os.environ.get("RTPT_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so"))
 _lib.pto_halton.restype = ctypes.c_float
 _lib.pto_halton.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
 _lib.pto_last_tests.restype = ctypes.c_uint64

@@ -13,6 +13,8 @@ import subprocess
 
 import pytest
 
+from conftest import native_toolchain
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -21,13 +23,13 @@ def checker(tmp_path_factory):
     cxx = shutil.which("g++") or shutil.which("c++")
     if cxx is None:
         pytest.skip("no C++ compiler")
-    lib = os.path.join(ROOT, "gpuraytracer_amd")
-    orc = os.path.join(ROOT, "oracle")
+    cxx, san, lib = native_toolchain(cxx)
+    orc = os.environ.get("RTPT_SAN_DIR") or os.path.join(ROOT, "oracle")
     if not os.path.exists(os.path.join(orc, "liboracle.so")):
         pytest.skip("oracle/liboracle.so not built")
     out = tmp_path_factory.mktemp("clu") / "cluster_check"
-    subprocess.check_call([cxx, "-std=c++17", "-O2", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
-                           "-I", os.path.join(lib, "csrc"),
+    subprocess.check_call([cxx, "-std=c++17", "-O2", "-ffp-contract=off", *san, "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "gpuraytracer_amd", "csrc"),
                            os.path.join(ROOT, "tests", "native", "cluster_check.cpp"),
                            "-L", lib, "-lrtpt", f"-Wl,-rpath,{lib}",
                            "-L", orc, "-loracle", f"-Wl,-rpath,{orc}", "-o", str(out)])

@@ -12,6 +12,8 @@ import subprocess
 
 import pytest
 
+from conftest import native_toolchain
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -21,9 +23,9 @@ def checker(tmp_path_factory):
     if cxx is None:
         pytest.skip("no C++ compiler")
     out = tmp_path_factory.mktemp("bvh") / "tri_bvh_check"
-    lib = os.path.join(ROOT, "gpuraytracer_amd")
-    subprocess.check_call([cxx, "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
-                           "-I", os.path.join(lib, "csrc"),
+    cxx, san, lib = native_toolchain(cxx)
+    subprocess.check_call([cxx, "-std=c++17", "-O2", *san, "-I", os.path.join(ROOT, "include"),
+                           "-I", os.path.join(ROOT, "gpuraytracer_amd", "csrc"),
                            os.path.join(ROOT, "tests", "native", "tri_bvh_check.cpp"),
                            "-L", lib, "-lrtpt", f"-Wl,-rpath,{lib}", "-o", str(out)])
     return str(out)
