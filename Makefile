@@ -14,7 +14,7 @@ HOSTCXX ?= /opt/rocm/llvm/bin/clang++
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-slp-vectorize $(EXTRA)
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -isystem /opt/rocm/include $(EXTRA)
 
-OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
+OBJS := $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_gsah.o $(BLD)/rt_api.o $(BLD)/rt_scene.o $(BLD)/rt_image.o
 HDRS := include/rtpt.h include/rt_types.h $(SRC)/rt_math.h $(SRC)/rt_kernel.hpp $(SRC)/rt_scene.hpp $(SRC)/rt_halton.hpp
 
 LIB ?= $(PKG)/librtpt.so
@@ -70,7 +70,7 @@ $(ASAN)/rt_api.o: $(SRC)/rt_api.cpp $(ALLSRC) | $(ASAN)
 $(ASAN)/%.o: $(SRC)/%.cpp $(HDRS) | $(ASAN)
 	$(HOSTCXX) $(HOSTFLAGS) $(SAN) -c $< -o $@
 
-$(ASAN)/librtpt.so: $(ASAN_HOST) $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o
+$(ASAN)/librtpt.so: $(ASAN_HOST) $(BLD)/rt_kernel.o $(BLD)/rt_mis.o $(BLD)/rt_lbvh.o $(BLD)/rt_gsah.o
 	$(HOSTCXX) -shared $(SAN) -o $@ $^ -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
 
 $(ASAN)/liboracle.so: oracle/pt_oracle.c oracle/pt_oracle.h include/rt_types.h | $(ASAN)

@@ -382,6 +382,12 @@ def main(argv=None, backend_factory=CudaBackend):
                                               "VALU instruction",
                            "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json, same "
                                      "kernel_src_sha) / live kernel time"}
+                lane = prof.get("valu_lane_utilization")
+                if lane:
+                    # useful lanes: issue fraction x the active lanes per issued
+                    # VALU instruction (SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU)
+                    compute["valu_lane_utilization"] = round(lane, 4)
+                    compute["lane_weighted_frac"] = round(wi / VALU_PEAK_WAVE_INSTR * lane, 4)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -411,6 +417,9 @@ def main(argv=None, backend_factory=CudaBackend):
                          "algorithmic_bytes_per_launch": launch_bytes},
             "compute_roofline": compute,
             "launch": launch,
+            # rt_create's scene build: which triangle-BVH build ran and how long
+            # it and the host scene compile took (outside the timed steps)
+            "build": (renderer.build_info() if hasattr(renderer, "build_info") else None),
             "step_ms_events": round(step_ms, 4),
             "kernel_ms_max_rank": round(kernel_ms_max, 4),
             "step_ms_max_rank": round(step_ms_max, 4),

@@ -104,7 +104,7 @@ assert ctypes.sizeof(CreateOptions) == 64
 # rt_scene_layout / rt_tri_bvh_build / rt_walk_scheduler (include/rtpt.h)
 LAYOUTS = {"auto": 0, "pairs": 1, "single": 2, "global": 3, "smem": 3, "pairsmem": 4, "sorted": 5, "bvh": 6}
 TRI_BUILDS = {"default": 0, "host": 1, "lbvh": 2, "gpusah": 3}
-WALKS = {"auto": 0, "lockstep": 1, "free": 2}
+WALKS = {"auto": 0, "lockstep": 1, "free": 2, "sorted": 3}
 
 RT_OK = 0
 RT_OUT_DEVICE, RT_OUT_FP16, RT_OUT_NONE, RT_KEEP_SUM, RT_OUT_RGBA8 = 0x1, 0x2, 0x4, 0x8, 0x10
@@ -122,6 +122,11 @@ class LaunchInfo(ctypes.Structure):  # rt_launch_info
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["kernel"] = self.kernel.decode()
         return d
+
+
+class BuildStats(ctypes.Structure):  # rt_build_stats
+    _fields_ = [("tri_bvh_build", ctypes.c_uint32), ("tri_bvh_nodes", ctypes.c_uint32),
+                ("tri_bvh_build_ms", ctypes.c_float), ("scene_compile_ms", ctypes.c_float)]
 
 
 class TileLayout(ctypes.Structure):  # rt_tile_layout_info
@@ -148,6 +153,7 @@ SIGNATURES = {
     "rt_last_kernel_ms": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     "rt_destroy": (ctypes.c_int, [_P]),
     "rt_last_launch": (ctypes.c_int, [_P, ctypes.POINTER(LaunchInfo)]),
+    "rt_build_info": (ctypes.c_int, [_P, ctypes.POINTER(BuildStats)]),
     "rt_comm_unique_id": (ctypes.c_int, [_P]),
     "rt_comm_init": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P]),
     "rt_render_gather": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <string>
 #include <vector>
@@ -41,6 +42,9 @@ struct rt_ctx {
     float4* d_tri_sorted = nullptr;
     uint32_t* d_tri_perm = nullptr;
     uint32_t tri_bvh_nodes = 0;      // per layout
+    uint32_t tri_bvh_build_used = 0; // rt_tri_bvh_build of the built tree (0: none)
+    float tri_bvh_build_ms = 0.0f;   // wall time of the triangle-BVH build
+    float scene_compile_ms = 0.0f;   // host scene compile (rt_scene.cpp compile_scene)
     float4* d_mis_shade = nullptr;
     float4* d_mis_tab = nullptr;   // Halton table of the MIS integrator
     uint32_t mis_tab_S = 0;        // samples per strategy it was built for
@@ -591,7 +595,7 @@ bool resolve_options(const rt_create_options* o, Resolved* r, const char** why) 
     r->lanes = o->lanes_per_pixel;
     switch (o->tri_bvh_build) {
         case RT_TRI_BVH_DEFAULT: r->tri_build = kDefaultTriBuild; break;
-        case RT_TRI_BVH_HOST_SAH: case RT_TRI_BVH_GPU_LBVH:
+        case RT_TRI_BVH_HOST_SAH: case RT_TRI_BVH_GPU_LBVH: case RT_TRI_BVH_GPU_SAH:
             r->tri_build = o->tri_bvh_build; break;
         default: *why = "rt_create_options.tri_bvh_build out of range"; return false;
     }
@@ -606,7 +610,7 @@ bool resolve_options(const rt_create_options* o, Resolved* r, const char** why) 
     if (o->sphere_leaf_max) r->build.sphere_leaf_max = o->sphere_leaf_max;
     if (o->sphere_median > 1) { *why = "rt_create_options.sphere_median must be 0 or 1"; return false; }
     r->build.sphere_sah = o->sphere_median == 0;
-    if (o->walk_scheduler > RT_WALK_FREE) { *why = "rt_create_options.walk_scheduler out of range"; return false; }
+    if (o->walk_scheduler > RT_WALK_SORTED) { *why = "rt_create_options.walk_scheduler out of range"; return false; }
     r->walk = o->walk_scheduler;
     return true;
 }
@@ -667,11 +671,14 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
     c->walk = ro.walk;
     DeviceGuard g(c->device);
     const char* err = nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t_compile = clk::now();
     if (!rt::compile_scene(*d->camera, d->materials, d->vertices, d->n_triangles,
                            d->square_lights[0], d->spheres, d->n_spheres, &c->scene, &err, ro.build)) {
         delete c;
         return fail(nullptr, RT_ERR_INVALID_ARG, err);
     }
+    c->scene_compile_ms = std::chrono::duration<float, std::milli>(clk::now() - t_compile).count();
     int status = RT_OK;
     std::string msg;
     do {
@@ -708,7 +715,22 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
                                            std::min(lds_pairs, lds_single) > rt::kMaxLdsBytes)));
         if (need_bvh) {
             const size_t nn = 2 * (size_t)nT - 1;
-            if (c->tri_build == RT_TRI_BVH_GPU_LBVH) {  // GPU Morton build (rt_lbvh.hip)
+            const auto t_build = clk::now();
+            if (c->tri_build == RT_TRI_BVH_GPU_SAH) {  // GPU binned SAH (rt_gsah.hip)
+                if ((e = hipMalloc((void**)&c->d_tri_nodes, rt::kTriCompactLayouts * nn * sizeof(uint4))) != hipSuccess ||
+                    (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
+                    (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
+                    status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;
+                }
+                uint32_t total = 0;
+                if ((e = rt::build_tri_gsah(c->d_tri_isect, nT, s.margin, ro.tri_leaf_max, ro.tri_leaf_cost,
+                                            c->d_tri_nodes, c->d_tri_sorted, c->d_tri_perm, &total,
+                                            c->stream)) != hipSuccess) {
+                    status = (e == hipErrorInvalidValue) ? RT_ERR_INVALID_ARG : RT_ERR_LAUNCH;
+                    msg = std::string("triangle BVH build: ") + hipGetErrorString(e); break;
+                }
+                c->tri_bvh_nodes = total;
+            } else if (c->tri_build == RT_TRI_BVH_GPU_LBVH) {  // GPU Morton build (rt_lbvh.hip)
                 if ((e = hipMalloc((void**)&c->d_tri_nodes, rt::kTriCompactLayouts * nn * sizeof(uint4))) != hipSuccess ||
                     (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
                     (e = hipMalloc((void**)&c->d_tri_perm, (size_t)nT * sizeof(uint32_t))) != hipSuccess) {
@@ -734,6 +756,8 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
                 c->tri_bvh_nodes = (uint32_t)(nodes.size() / (4 * rt::kTriCompactLayouts));
             }
             if (c->tri_build == RT_TRI_BVH_GPU_LBVH) c->tri_bvh_nodes = (uint32_t)nn;
+            c->tri_bvh_build_used = c->tri_build;
+            c->tri_bvh_build_ms = std::chrono::duration<float, std::milli>(clk::now() - t_build).count();
         }
         const size_t npx = (size_t)s.cam.W * (size_t)s.cam.H;
         if ((e = hipMalloc((void**)&c->d_seeds, npx * sizeof(uint32_t))) != hipSuccess) {
@@ -889,6 +913,16 @@ int rt_place_tiles_host(const void* gathered, int32_t width, int32_t height, int
             memcpy(static_cast<char*>(frame) + (size_t)(k + j * N) * L.row_bytes,
                    static_cast<const char*>(gathered) + k * L.tile_bytes + j * L.row_bytes, L.row_bytes);
     }
+    return RT_OK;
+}
+
+int rt_build_info(const rt_ctx* c, rt_build_stats* info) {
+    if (!c || !info) return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
+    memset(info, 0, sizeof(*info));
+    info->tri_bvh_build = c->tri_bvh_build_used;
+    info->tri_bvh_nodes = c->tri_bvh_nodes;
+    info->tri_bvh_build_ms = c->tri_bvh_build_ms;
+    info->scene_compile_ms = c->scene_compile_ms;
     return RT_OK;
 }
 

@@ -251,8 +251,29 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
         leaf = kNone;
     };
 
+#ifdef RT_STATS
+    // free-kernel counters (tools/free_stats.py): [0] waves, [1] service
+    // phases, [2] lanes served, [3] live lanes at service, [4] walk steps,
+    // [5] lanes stepping, [6] leaf rounds, [7] lanes in leaf rounds, [8]
+    // cycles in service, [9] cycles in walk phases, [10] queries started
+    RT_STAT(0, 1);
+    unsigned long long t_ph = clock64();
+#endif
     for (;;) {
         // ---------------- service phase ----------------
+#ifdef RT_STATS
+        RT_STAT(1, 1);
+        RT_STAT(2, __popcll(__ballot(ph <= kFpShadow ? idx >= end : ph == kFpEnd)));
+        RT_STAT(3, __popcll(__ballot(ph != kFpDone)));
+        {
+            const unsigned long long t1 = clock64();
+            RT_STAT(9, t1 - t_ph);
+            t_ph = t1;
+        }
+#endif
+        // a leaf parked at the end of its walk (the walk phase may stop before
+        // the parked leaves reach their round)
+        if (leaf != kNone) resolve_leaf();
         const bool fin = ph <= kFpShadow && idx >= end;
         // (1) a finished shadow query: raytrace.metal:79-89, then the next bounce (:99-100)
         if (fin && ph == kFpShadow) {
@@ -385,8 +406,16 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
             end = idx + nLay;
             if (id >= 0 && shadow) idx = end;                      // occluded by a wall
             ph = shadow ? kFpShadow : kFpClosest;
+            RT_STAT(10, __popcll(__ballot(1)));
         }
         const bool live = ph != kFpDone;
+#ifdef RT_STATS
+        {
+            const unsigned long long t1 = clock64();
+            RT_STAT(8, t1 - t_ph);
+            t_ph = t1;
+        }
+#endif
         if (__builtin_amdgcn_ballot_w64(live) == 0) break;
         // ---------------- walk phase ----------------
         // Lanes take BVH steps; a lane that meets a leaf worth testing parks it
@@ -397,6 +426,8 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
         const int nlive = __popcll(__builtin_amdgcn_ballot_w64(live));
         for (;;) {
             const bool adv = live && idx < end && leaf == kNone;
+            RT_STAT(4, 1);
+            RT_STAT(5, __popcll(__ballot(adv)));
             if (adv) {
                 if constexpr (SPH) {
                     const uint4 e = sv.sent[idx];
@@ -429,7 +460,30 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
             const int np = __popcll(__builtin_amdgcn_ballot_w64(parked));
             const int nwalk = __popcll(__builtin_amdgcn_ballot_w64(parked || (live && idx < end)));
             if (np > 0 && kLeafDen * np >= nwalk) {
-                if (parked) resolve_leaf();
+                RT_STAT(6, 1);
+                RT_STAT(7, np);
+                if constexpr (SPH) {
+                    // every lane evaluates the roots, parked lanes keep the
+                    // result: the branch form (resolve_leaf under `if (parked)`)
+                    // measured 4 wrong values in 13,824 on 1000 spheres x 9 spp
+                    // (tests/test_gpu_free.py) where this select form and the
+                    // lockstep walk are bit-exact -- not understood, kept out
+                    const float sq = sqrtf(parked ? pdisc : 1.0f);
+                    const float a2 = 2.0f * a;
+                    float t = (-pb - sq) / a2;
+                    const float t2 = (-pb + sq) / a2;
+                    t = (t > tmin) ? t : t2;
+                    const int sidv = (int)(sv.nT + sv.sid[parked ? leaf : 0u]);
+                    const bool sh = ph == kFpShadow;
+                    const bool hit_any = sh && t > tmin && t < best;
+                    const bool hit_c = !sh && t > tmin && t < 3.0e38f && t <= best && (t < best || sidv < id);
+                    id = (parked && hit_any) ? 0 : ((parked && hit_c) ? sidv : id);
+                    idx = (parked && hit_any) ? end : idx;
+                    best = (parked && hit_c) ? t : best;
+                    leaf = kNone;
+                } else {
+                    if (parked) resolve_leaf();
+                }
             }
             const int nfin = nlive - __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone || (live && idx < end)));
             if (kFreeParkDen * nfin >= nlive) break;

@@ -343,24 +343,29 @@ __device__ __forceinline__ void deliver(float4* lds, uint32_t owner, f3 acc) {
     sum[2 * kBlockThreads + owner] = sum[2 * kBlockThreads + owner] + acc.z;
 }
 
-template <int b, int B, bool SPH, bool SMALL>
+// GEO: kGeoPairLds (pair records in LDS, wave-culled loops), kGeoTriBvh
+// (triangle BVH: camera rays as wave packets, bounce rays per lane) or
+// kGeoSphLds (the room's pairs in LDS + the compact sphere BVH).  For the BVH
+// scenes the sort is what the lockstep kernels lack: the waves of a bounce
+// walk rays of ONE direction octant, i.e. ONE of the eight BVH layouts.
+template <int b, int B, int GEO, bool SPH, bool SMALL>
 struct SortedChain {
     __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv, float4* lds,
                                                PathState& s, uint32_t& owner, bool& alive) {
         if (b > 0) sort_paths(lds, s, owner, alive);
         if (alive) {
             float t = 1000.0f;                                   // sampling.metal:154-155
-            const int id = closest_hit<kGeoPairLds, SPH, true, (b == 0 ? 0 : 1)>(sv, s.o, s.d,
-                                                                               0.001f, &t);
+            constexpr bool cull = GEO == kGeoTriBvh ? b == 0 : true;
+            const int id = closest_hit<GEO, SPH, cull, (b == 0 ? 0 : 1)>(sv, s.o, s.d, 0.001f, &t);
             if (b > 0) load_thr_acc(lds, s);
-            alive = id >= 0 && shade<b, B, kGeoPairLds, SPH, SMALL>(P, sv, s, id, t);
+            alive = id >= 0 && shade<b, B, GEO, SPH, SMALL>(P, sv, s, id, t);
             if (!alive || b + 1 == B) deliver(lds, owner, s.acc);
         }
-        SortedChain<b + 1, B, SPH, SMALL>::run(P, sv, lds, s, owner, alive);
+        SortedChain<b + 1, B, GEO, SPH, SMALL>::run(P, sv, lds, s, owner, alive);
     }
 };
-template <int B, bool SPH, bool SMALL>
-struct SortedChain<B, B, SPH, SMALL> {
+template <int B, int GEO, bool SPH, bool SMALL>
+struct SortedChain<B, B, GEO, SPH, SMALL> {
     __device__ __forceinline__ static void run(const KParams&, const SceneView&, float4*,
                                                PathState&, uint32_t&, bool&) {}
 };
@@ -606,18 +611,28 @@ void path_trace_kernel(KParams P) {
 
 #include "rt_free.hpp"
 
-template <int B, bool SPH, bool SMALL>
-__global__ __launch_bounds__(kBlockThreads, kMinWavesPerEu) void path_trace_sorted_kernel(
+// waves per SIMD of the sorted kernel: the pair layout keeps 8; the BVH walks
+// hold more state (RTPT A/B: sorted_waves)
+#ifndef RT_SORTED_BVH_WAVES
+#define RT_SORTED_BVH_WAVES 4
+#endif
+template <int B, int GEO, bool SPH, bool SMALL>
+__global__ __launch_bounds__(kBlockThreads, GEO == kGeoPairLds ? kMinWavesPerEu : RT_SORTED_BVH_WAVES)
+void path_trace_sorted_kernel(
     KParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
     sv.nT = P.nT;
     sv.nP = P.nP;
     sv.nS = SPH ? P.nS : 0u;
-    const uint32_t ng4 = kPairF4 * sv.nP;
+    sv.nC = 0;
+    sv.htab = nullptr;
+    const uint32_t ng4 = GEO == kGeoTriBvh ? 0u : kPairF4 * sv.nP;
     float4* scene = lds + kSortF4;  // sort buffers first: compile-time offsets
     for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) scene[k] = P.pair_isect[k];
-    sv.nN = SPH ? P.nN : 0u;
+    sv.nN = SPH ? (GEO == kGeoSphLds ? P.nE : P.nN) : 0u;
+    sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
+    sv.sid = P.sph_lds_id;
     sv.tnode = P.tri_nodes;
     sv.tsorted = P.tri_sorted;
     sv.tperm = P.tri_perm;
@@ -661,7 +676,7 @@ __global__ __launch_bounds__(kBlockThreads, kMinWavesPerEu) void path_trace_sort
         }
         uint32_t owner = tid;
         bool alive = valid;
-        SortedChain<0, B, SPH, SMALL>::run(P, sv, lds, s, owner, alive);
+        SortedChain<0, B, GEO, SPH, SMALL>::run(P, sv, lds, s, owner, alive);
         __syncthreads();  // sample n's hand-offs land before sample n+1's
     }
     if (!valid) return;
@@ -750,6 +765,8 @@ inline int lanes_per_pixel(const KParams& P, int geo) {
 constexpr int kGeoPairSorted = 3;  // pair records + per-bounce octant sort of the paths
 constexpr int kGeoFreeSph = 8;     // free-running lanes, sphere scene (rt_free.hpp)
 constexpr int kGeoFreeTri = 9;     // free-running lanes, triangle BVH
+constexpr int kGeoSortSph = 10;    // octant-sorted paths, sphere scene
+constexpr int kGeoSortTri = 11;    // octant-sorted paths, triangle BVH
 
 // The most recent launch of this thread (launch_path_trace copies it out).
 thread_local LaunchInfo g_last;
@@ -831,14 +848,30 @@ hipError_t launch_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
                  : launch_t<B, GEO, false, false>(P, lds_bytes, stream);
 }
 
-template <int B, bool SPH, bool SMALL>
+template <int B, int GEO, bool SPH, bool SMALL>
 hipError_t launch_sorted_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     const dim3 grid((P.W + kTile - 1) / kTile, (P.row_count + kTile - 1) / kTile);
-    note_launch<B, kGeoPairSorted, SPH, SMALL, 1>("path_trace_sorted_kernel", P, grid, kBlockThreads,
-                                                   lds_bytes);
-    hipLaunchKernelGGL((path_trace_sorted_kernel<B, SPH, SMALL>), grid, dim3(kBlockThreads),
+    note_launch<B, GEO, SPH, SMALL, 1>("path_trace_sorted_kernel", P, grid, kBlockThreads, lds_bytes);
+    hipLaunchKernelGGL((path_trace_sorted_kernel<B, GEO, SPH, SMALL>), grid, dim3(kBlockThreads),
                        lds_bytes, stream, P);
     return hipGetLastError();
+}
+
+template <int B, int GEO>
+hipError_t launch_sorted_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
+    const bool small = P.max_index < kSmallIndexMax;
+    const size_t bytes = (GEO == kGeoTriBvh ? 0 : lds_bytes) + sorted_lds_extra_bytes();
+    if constexpr (GEO == kGeoSphLds)
+        return small ? launch_sorted_t<B, GEO, true, true>(P, bytes, stream)
+                     : launch_sorted_t<B, GEO, true, false>(P, bytes, stream);
+    if constexpr (GEO == kGeoTriBvh)
+        return small ? launch_sorted_t<B, GEO, false, true>(P, bytes, stream)
+                     : launch_sorted_t<B, GEO, false, false>(P, bytes, stream);
+    if (P.nS > 0)
+        return small ? launch_sorted_t<B, GEO, true, true>(P, bytes, stream)
+                     : launch_sorted_t<B, GEO, true, false>(P, bytes, stream);
+    return small ? launch_sorted_t<B, GEO, false, true>(P, bytes, stream)
+                 : launch_sorted_t<B, GEO, false, false>(P, bytes, stream);
 }
 
 // The free-running kernel (rt_free.hpp): one pixel per lane, 8x8-pixel waves
@@ -869,15 +902,9 @@ template <int B>
 hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t stream) {
     if (geo == kGeoFreeSph) return launch_free<B, kGeoSphLds>(P, lds_bytes, stream);
     if (geo == kGeoFreeTri) return launch_free<B, kGeoTriBvh>(P, lds_bytes, stream);
-    if (geo == kGeoPairSorted) {
-        const bool small = P.max_index < kSmallIndexMax;
-        const size_t bytes = lds_bytes + sorted_lds_extra_bytes();
-        if (P.nS > 0)
-            return small ? launch_sorted_t<B, true, true>(P, bytes, stream)
-                         : launch_sorted_t<B, true, false>(P, bytes, stream);
-        return small ? launch_sorted_t<B, false, true>(P, bytes, stream)
-                     : launch_sorted_t<B, false, false>(P, bytes, stream);
-    }
+    if (geo == kGeoPairSorted) return launch_sorted_g<B, kGeoPairLds>(P, lds_bytes, stream);
+    if (geo == kGeoSortSph) return launch_sorted_g<B, kGeoSphLds>(P, lds_bytes, stream);
+    if (geo == kGeoSortTri) return launch_sorted_g<B, kGeoTriBvh>(P, lds_bytes, stream);
     switch (geo) {
         case kGeoPairLds: return launch_g<B, kGeoPairLds>(P, lds_bytes, stream);
         case kGeoPairClu: return launch_g<B, kGeoPairClu>(P, lds_bytes, stream);
@@ -933,10 +960,17 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
         if (geo == kGeoSphLds) geo = kGeoFreeSph;
         if (geo == kGeoTriBvh && P.nS == 0) geo = kGeoFreeTri;
     }
+    // octant-sorted paths for BVH scenes (rt_create_options.walk_scheduler)
+    if (P.walk == kWalkSorted) {
+        if (geo == kGeoSphLds) geo = kGeoSortSph;
+        if (geo == kGeoTriBvh && P.nS == 0) geo = kGeoSortTri;
+    }
 #ifdef RT_DEV_ISA  // ISA-inspection builds only (tools/isa.sh): the two headline layouts at B = 3
     if (bounces != 3) return hipErrorInvalidValue;
     if (geo == kGeoFreeSph) return launch_free<3, kGeoSphLds>(P, lds_total, stream);
     if (geo == kGeoFreeTri) return launch_free<3, kGeoTriBvh>(P, lds_total, stream);
+    if (geo == kGeoSortSph) return launch_sorted_g<3, kGeoSphLds>(P, lds_total, stream);
+    if (geo == kGeoSortTri) return launch_sorted_g<3, kGeoTriBvh>(P, lds_total, stream);
     return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_total, stream)
                               : launch_g<3, kGeoSphLds>(P, lds_total, stream);
 #endif

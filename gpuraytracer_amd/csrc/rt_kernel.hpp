@@ -67,7 +67,7 @@ struct KParams {
     uint32_t flags;
     uint32_t max_index;       // max Halton index seed+n of this launch (0xFFFFFFFF: unknown/wraps)
     uint32_t lanes;           // lanes per pixel: 0 = auto, else 1, 4 or 16 (rt_create_options)
-    uint32_t walk;            // rt_walk_scheduler: 0 auto, 1 lockstep, 2 free-running lanes
+    uint32_t walk;            // rt_walk_scheduler: 0 auto, 1 lockstep, 2 free-running lanes, 3 sorted
     uint32_t wave_w;          // pixels per wave row (set by the launcher)
     const float4* clusters;   // box clusters, kCluF4 float4 each, or null
     uint32_t nC;              // clusters (0: none)
@@ -82,7 +82,7 @@ struct LaunchInfo {
 };
 // Where the workgroup reads the intersection records from.
 // rt_walk_scheduler (include/rtpt.h)
-constexpr uint32_t kWalkAuto = 0, kWalkLockstep = 1, kWalkFree = 2;
+constexpr uint32_t kWalkAuto = 0, kWalkLockstep = 1, kWalkFree = 2, kWalkSorted = 3;
 enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5, kPairLds = 6 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream,
                              LaunchInfo* info);
@@ -119,6 +119,17 @@ size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs);
 hipError_t build_tri_lbvh(const float4* d_tri, uint32_t n, const float lo[3], const float hi[3],
                           float margin, uint4* d_nodes, float4* d_sorted, uint32_t* d_perm,
                           hipStream_t s);
+
+// GPU binned-SAH build of the triangle BVH (rt_gsah.hip): the host build's
+// rules (32 bins, SAH leaf rule) level by level on the device, written in the
+// same compact layout.  d_nodes: 8 * (2n-1) uint4 at most, d_sorted: 3n
+// float4, d_perm: n; *total_nodes = nodes per layout.  Synchronises the stream.
+hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_t leaf_max, double trav_cost,
+                          uint4* d_nodes, float4* d_sorted, uint32_t* d_perm, uint32_t* total_nodes,
+                          hipStream_t s);
+// Deterministic exclusive scan of n uint32 (rt_gsah.hip); tile_sums holds
+// ceil(n / 1024) words.
+hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tile_sums, hipStream_t s);
 
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
 

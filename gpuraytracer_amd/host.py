@@ -20,7 +20,7 @@ import numpy as np
 
 from ._native import (LAYOUTS, RT_COMM_ID_BYTES, RT_KEEP_SUM, RT_OK, RT_OUT_DEVICE, RT_OUT_FP16,
                       RT_OUT_NONE, RT_OUT_RGBA8, TRI_BUILDS, WALKS,
-                      CameraGPU, CreateOptions, LaunchInfo, MaterialGPU, MisParamsC, RenderParamsC,
+                      BuildStats, CameraGPU, CreateOptions, LaunchInfo, MaterialGPU, MisParamsC, RenderParamsC,
                       RtError, SceneDesc, SceneInfo, SphereGPU, SquareLightGPU, TileLayout, float3,
                       lib)
 
@@ -531,6 +531,14 @@ class Renderer:
         info = LaunchInfo()
         _check(lib.rt_last_launch(self._ctx, ctypes.byref(info)), self._ctx)
         return info.as_dict()
+
+    def build_info(self) -> dict:
+        """rt_build_info: which triangle-BVH build ran (0 none, 1 host SAH, 2 GPU
+        LBVH, 3 GPU SAH), its nodes per layout and the build / scene-compile
+        wall times in ms."""
+        b = BuildStats()
+        _check(lib.rt_build_info(self._ctx, ctypes.byref(b)), self._ctx)
+        return {k: getattr(b, k) for k, _ in BuildStats._fields_}
 
     def last_kernel_ms(self) -> float:
         ms = ctypes.c_float()

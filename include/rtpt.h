@@ -127,9 +127,13 @@ typedef enum rt_tri_bvh_build {
 typedef enum rt_walk_scheduler {
     RT_WALK_AUTO = 0,          /* measured best per scene                            */
     RT_WALK_LOCKSTEP = 1,      /* a wave's lanes run each bounce's queries together  */
-    RT_WALK_FREE = 2           /* every lane runs its own path state; lanes whose
+    RT_WALK_FREE = 2,          /* every lane runs its own path state; lanes whose
                                   walk ended park until half the wave has, then
                                   shade and start their next query together        */
+    RT_WALK_SORTED = 3         /* between bounces the paths of a workgroup are
+                                  counting-sorted by direction octant (ballots),
+                                  finished paths dropped: a wave walks one BVH
+                                  layout                                           */
 } rt_walk_scheduler;
 
 typedef struct rt_create_options {
@@ -255,6 +259,17 @@ typedef struct rt_launch_info {
     uint32_t lds_bytes;         /* dynamic LDS per workgroup                      */
 } rt_launch_info;
 int rt_last_launch(const rt_ctx* ctx, rt_launch_info* info);
+
+/* How rt_create built the scene: which triangle-BVH build ran (rt_tri_bvh_build,
+ * 0 = no triangle BVH), its nodes per octant layout, and the wall times of the
+ * build (device sync / upload included) and of the host scene compile. */
+typedef struct rt_build_stats {
+    uint32_t tri_bvh_build;
+    uint32_t tri_bvh_nodes;
+    float tri_bvh_build_ms;
+    float scene_compile_ms;
+} rt_build_stats;
+int rt_build_info(const rt_ctx* ctx, rt_build_stats* info);
 
 /* Hash of the sources this library was built from (gpuraytracer_amd/srchash.py:
  * csrc/ + include/): a loader can refuse a stale binary. */

@@ -426,7 +426,10 @@ TRI_BUILD_OPTIONS = {
     # leaves of up to 4 triangles (word first | (count - 1) << 24): the count > 1
     # loops of tri_leaf_closest / tri_leaf_any in the packet and parked-leaf walks
     "host_leaf4": Options(tri_build="host", tri_leaf_max=4, tri_leaf_cost=2.0),
+    "gpusah": Options(tri_build="gpusah"),
+    "gpusah_leaf4": Options(tri_build="gpusah", tri_leaf_max=4, tri_leaf_cost=2.0),
 }
+BUILD_CODE = {"host": 1, "lbvh": 2, "gpusah": 3}
 
 
 @pytest.mark.parametrize("build", list(TRI_BUILD_OPTIONS))
@@ -440,6 +443,10 @@ def test_triangle_bvh_gpu_build_bit_exact(n, dup, build):
     sd = seed_splitmix(40, 24)
     with Renderer(s, seeds=sd, options=TRI_BUILD_OPTIONS[build]) as r:
         out = r.render(RenderParams(spp=2, bounces=3))
+        info = r.build_info()
+    assert info["tri_bvh_build"] == BUILD_CODE[build.split("_")[0]], info
+    total = 2 * (n + 36) - 1
+    assert (info["tri_bvh_nodes"] == total) if "leaf4" not in build else (info["tri_bvh_nodes"] < total), info
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"soup{n}")
 
 

@@ -10,5 +10,5 @@ mkdir -p "$R/abvar" "$R/build_a"
     -I"$R/gpuraytracer_amd/csrc" --offload-arch=gfx950 -fno-slp-vectorize "$@" \
     -c "$R/gpuraytracer_amd/csrc/rt_kernel.hip" -o "$R/build_a/rt_kernel_$N.o"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/abvar/librtpt_$N.so" "$R/build_a/rt_kernel_$N.o" \
-    "$R/build/rt_mis.o" "$R/build/rt_lbvh.o" "$R/build/rt_api.o" "$R/build/rt_scene.o" \
+    "$R/build/rt_mis.o" "$R/build/rt_lbvh.o" "$R/build/rt_gsah.o" "$R/build/rt_api.o" "$R/build/rt_scene.o" \
     "$R/build/rt_image.o" -L/opt/rocm/lib -lrccl

@@ -15,7 +15,7 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ne 0 ]; then echo "[r5] $name failed rc=$rc" >&2; tail -30 "$OUT/$name.err" >&2; tail -30 "$OUT/$name.out" >&2; exit $rc; fi
 }
 step tests_free 400 python -u -m pytest tests/test_gpu_free.py -x -v --timeout 300 --timeout-method thread
-for w in lockstep free; do
+for w in ${WALKS:-lockstep free}; do
   step sph_$w 200 env RTPT_WALK=$w python bench.py --scene spheres --steps 6 --warmup 1 --cpu-baseline off
   step tri_$w 300 env RTPT_WALK=$w python bench.py --scene triangles --triangles 100000 --spp 64 --steps 4 --warmup 1 --cpu-baseline off
 done
