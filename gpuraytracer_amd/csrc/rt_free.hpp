@@ -252,22 +252,23 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
     };
 
 #ifdef RT_STATS
-    // free-kernel counters (tools/free_stats.py): [0] waves, [1] service
-    // phases, [2] lanes served, [3] live lanes at service, [4] walk steps,
-    // [5] lanes stepping, [6] leaf rounds, [7] lanes in leaf rounds, [8]
-    // cycles in service, [9] cycles in walk phases, [10] queries started
-    RT_STAT(0, 1);
+    // free-kernel counters (tools/free_stats.py), slots 16 + : [0] waves, [1]
+    // service phases, [2] lanes served, [3] live lanes at service, [4] walk
+    // steps, [5] lanes stepping, [6] leaf rounds, [7] lanes in leaf rounds,
+    // [8] cycles in service, [9] cycles in walk phases, [10] queries started
+    // (slots 0-15 are the pair loops' counters)
+    RT_STAT(16, 1);
     unsigned long long t_ph = clock64();
 #endif
     for (;;) {
         // ---------------- service phase ----------------
 #ifdef RT_STATS
-        RT_STAT(1, 1);
-        RT_STAT(2, __popcll(__ballot(ph <= kFpShadow ? idx >= end : ph == kFpEnd)));
-        RT_STAT(3, __popcll(__ballot(ph != kFpDone)));
+        RT_STAT(17, 1);
+        RT_STAT(18, __popcll(__ballot(ph <= kFpShadow ? idx >= end : ph == kFpEnd)));
+        RT_STAT(19, __popcll(__ballot(ph != kFpDone)));
         {
             const unsigned long long t1 = clock64();
-            RT_STAT(9, t1 - t_ph);
+            RT_STAT(25, t1 - t_ph);
             t_ph = t1;
         }
 #endif
@@ -406,13 +407,13 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
             end = idx + nLay;
             if (id >= 0 && shadow) idx = end;                      // occluded by a wall
             ph = shadow ? kFpShadow : kFpClosest;
-            RT_STAT(10, __popcll(__ballot(1)));
+            RT_STAT(26, __popcll(__ballot(1)));
         }
         const bool live = ph != kFpDone;
 #ifdef RT_STATS
         {
             const unsigned long long t1 = clock64();
-            RT_STAT(8, t1 - t_ph);
+            RT_STAT(24, t1 - t_ph);
             t_ph = t1;
         }
 #endif
@@ -426,8 +427,8 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
         const int nlive = __popcll(__builtin_amdgcn_ballot_w64(live));
         for (;;) {
             const bool adv = live && idx < end && leaf == kNone;
-            RT_STAT(4, 1);
-            RT_STAT(5, __popcll(__ballot(adv)));
+            RT_STAT(20, 1);
+            RT_STAT(21, __popcll(__ballot(adv)));
             if (adv) {
                 if constexpr (SPH) {
                     const uint4 e = sv.sent[idx];
@@ -460,8 +461,8 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
             const int np = __popcll(__builtin_amdgcn_ballot_w64(parked));
             const int nwalk = __popcll(__builtin_amdgcn_ballot_w64(parked || (live && idx < end)));
             if (np > 0 && kLeafDen * np >= nwalk) {
-                RT_STAT(6, 1);
-                RT_STAT(7, np);
+                RT_STAT(22, 1);
+                RT_STAT(23, np);
                 if constexpr (SPH) {
                     // every lane evaluates the roots, parked lanes keep the
                     // result: the branch form (resolve_leaf under `if (parked)`)

@@ -41,7 +41,9 @@ struct PathState {
 // FUSE (pair layout, triangles only): the shadow query of bounce b and the
 // closest hit of bounce b+1 run as one pass over the records
 // (fused_shadow_closest); the next hit is returned in *nid / *nt.
-template <int b, int B, int GEO, bool SPH, bool SMALL, bool FUSE = false>
+// STASH (the one-wave sphere kernel): contrib and the next direction wait in
+// the per-lane LDS stash sv.xstash across the shadow walk.
+template <int b, int B, int GEO, bool SPH, bool SMALL, bool FUSE = false, bool STASH = false>
 __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, PathState& s, int id,
                                       float t, int* nid = nullptr, float* nt = nullptr) {
     f3 N, right, fwd, diffuse;
@@ -121,6 +123,33 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     // every lane (skipping there: 100k triangles -8 %).
     const bool lit = (GEO == kGeoTriBvh && b == 0) || contrib.x != 0.0f || contrib.y != 0.0f ||
                      contrib.z != 0.0f;
+    if constexpr (STASH) {
+        // the sphere kernel parks contrib and the next direction in a per-lane
+        // LDS stash across the shadow walk (read back through an opaque lane
+        // index, so they are not kept in registers): at 64 VGPRs (8 waves/SIMD)
+        // they were 5 spilled VGPRs, 24 B of scratch per lane (round 4)
+        uint32_t t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        float* st = sv.xstash;
+        st[t] = contrib.x;
+        st[kSphBlockThreads + t] = contrib.y;
+        st[2 * kSphBlockThreads + t] = contrib.z;
+        if (b + 1 < B) {
+            st[3 * kSphBlockThreads + t] = d2.x;
+            st[4 * kSphBlockThreads + t] = d2.y;
+            st[5 * kSphBlockThreads + t] = d2.z;
+        }
+        const bool occluded = lit && any_hit<GEO, SPH, false>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi);
+        uint32_t t2 = threadIdx.x;
+        asm volatile("" : "+v"(t2));
+        if (lit && !occluded)                              // :79-89
+            s.acc = s.acc + f3{st[t2], st[kSphBlockThreads + t2], st[2 * kSphBlockThreads + t2]};
+        if (b + 1 < B) {
+            s.d = f3{st[3 * kSphBlockThreads + t2], st[4 * kSphBlockThreads + t2], st[5 * kSphBlockThreads + t2]};
+            s.o = p;                                       // :99-100
+        }
+        return true;
+    }
     if (lit && !any_hit<GEO, SPH, b == 0 && !SPH>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + contrib;                           // :87-89
     if (b + 1 < B) {
@@ -137,7 +166,7 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     // Camera rays of an 8x8 tile are coherent: cull with their segment boxes.
     const int id = closest_hit<GEO, SPH, b == 0, (b == 0 ? 0 : 1)>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
     if (id < 0) return false;                               // :51-53
-    return shade<b, B, GEO, SPH, SMALL>(P, sv, s, id, t);
+    return shade<b, B, GEO, SPH, SMALL, false, GEO == kGeoSphLds>(P, sv, s, id, t);
 }
 
 template <int b, int B, int GEO, bool SPH, bool SMALL>
@@ -424,6 +453,8 @@ void path_trace_kernel(KParams P) {
         if (GEO == kGeoSphLds) {  // the compact sphere BVH (8 layouts) stays in global memory (L2)
             sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
             sv.sid = P.sph_lds_id;
+            __shared__ float sph_stash[GEO == kGeoSphLds ? 6 * kSphBlockThreads : 1];
+            sv.xstash = sph_stash;
         }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
@@ -553,7 +584,10 @@ void path_trace_kernel(KParams P) {
         }
         if (L == 1) {
             lum = lum + s.acc;                                   // :103
-        } else if (L <= 16 && !SPH) {
+#ifndef RT_SPH_DPP
+#define RT_SPH_DPP 0
+#endif
+        } else if (L <= 16 && (!SPH || RT_SPH_DPP)) {
             // a pixel's L lanes are consecutive lanes of one 16-lane DPP row
             // (L = 4: groups at 0, 4, 8, 12; L = 16: the whole row), so its
             // leader reads sample r*L + k from lane +k with a row shift fused

@@ -379,7 +379,11 @@ constexpr uint32_t kMisRowPixels = 64u / kMisLanes;
 // dl/dc and the running strategy sum wait in the per-lane LDS stash (round 2:
 // 120 VGPRs at 4 waves; 6 waves then spilled 54 VGPRs).  DESIGN.md §5
 constexpr int kMisWavesPerEu = 7;
-template <int GEO>
+// FREEP: the scene has pairs in no box cluster (P.pair_free != 0).  The
+// reference scene has none; with FREEP false their loop is compiled out, which
+// also drops the one VGPR its loop-invariant test occupied (8 B of scratch at
+// 7 waves/SIMD, round 4).
+template <int GEO, bool FREEP = true>
 __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
@@ -415,7 +419,7 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
         sv.pair = lds;
         sv.clu = lds + ng4;
         sv.nC = P.nC;
-        sv.pair_free = P.pair_free;
+        sv.pair_free = FREEP ? P.pair_free : 0u;
     } else {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
@@ -563,16 +567,16 @@ size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + sha
 // fit the 64 KB of the LDS layouts keeps them with the 15 KB stash on top
 // (up to 79 KB per workgroup, fewer workgroups per CU) instead of dropping to
 // the global-memory kernel.
-template <int GEO>
+template <int GEO, bool FREEP = true>
 hipError_t launch_mis_g(const MisParams& P, size_t lds, hipStream_t stream) {
     constexpr uint32_t TX = kMisTile ? 16u : kMisRowPixels, TY = kMisTile ? 2u * (8u / kMisLanes) : 4u;
     const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);  // workgroup: TX x TY pixels
     if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute((const void*)mis_kernel<GEO>,
+        const hipError_t e = hipFuncSetAttribute((const void*)mis_kernel<GEO, FREEP>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(mis_kernel<GEO>, grid, dim3(kBlockThreads), lds, stream, P);
+    hipLaunchKernelGGL((mis_kernel<GEO, FREEP>), grid, dim3(kBlockThreads), lds, stream, P);
     return hipGetLastError();
 }
 
@@ -585,7 +589,8 @@ hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {
     if (!lds_ok) return launch_mis_g<kGeoTriGlobal>(P, X, stream);
     const size_t lds_clu = lds + kCluF4 * P.nC * sizeof(float4);
     if (pairs && P.nC > 0 && mem == SceneMem::kAuto && lds_clu <= kMaxLdsBytes)
-        return launch_mis_g<kGeoPairClu>(P, lds_clu + X, stream);
+        return P.pair_free ? launch_mis_g<kGeoPairClu, true>(P, lds_clu + X, stream)
+                           : launch_mis_g<kGeoPairClu, false>(P, lds_clu + X, stream);
     if (pairs) return launch_mis_g<kGeoPairLds>(P, lds + X, stream);
     return launch_mis_g<kGeoTriLds>(P, lds + X, stream);
 }

@@ -17,8 +17,9 @@ scene = (Scene.random_spheres(W, H, 1000, seed=42) if kind == "spheres"
          else Scene.random_triangles(W, H, 100_000))
 with Renderer(scene, options=Options(walk="free")) as r:
     r.render(RenderParams(spp=SPP, bounces=3))
-    st = (ctypes.c_uint64 * 32)()
-    assert lib.rt_debug_stats(r._ctx, st, 32) == 0, lib.rt_last_error(r._ctx)
+    st0 = (ctypes.c_uint64 * 32)()
+    assert lib.rt_debug_stats(r._ctx, st0, 32) == 0, lib.rt_last_error(r._ctx)
+    st = list(st0)[16:]
     kernel = r.last_launch()["kernel"]
 waves = max(st[0], 1)
 samples = W * H * SPP
