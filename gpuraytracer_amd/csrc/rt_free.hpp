@@ -30,7 +30,15 @@
 // next direction and the pixel sum in a per-lane LDS stash (read and written
 // only in the service phase, so they are not live across the walk loop).
 
-constexpr int kFreeParkDen = 2;  // service once >= 1/2 of the live lanes finished their query
+// service once >= kFreeParkNum/kFreeParkDen of the live lanes finished their
+// query (1/2 measured best of 1/4, 1/3, 1/2, 2/3, 3/4)
+#ifndef RT_FREE_PARK_DEN
+#define RT_FREE_PARK_DEN 2
+#endif
+#ifndef RT_FREE_PARK_NUM
+#define RT_FREE_PARK_NUM 1
+#endif
+constexpr int kFreeParkDen = RT_FREE_PARK_DEN, kFreeParkNum = RT_FREE_PARK_NUM;
 
 // stash slots (floats, SoA: slot * 64 + lane)
 enum FreeSlot : int {
@@ -122,7 +130,11 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
     constexpr bool SPH = GEO == kGeoSphLds;
     // parked leaves are tested once they are >= 1/kLeafDen of the walking lanes
     // (the lockstep walks' kSphParkDen / kTriParkDen)
+#ifdef RT_FREE_LEAF_DEN
+    constexpr int kLeafDen = RT_FREE_LEAF_DEN;
+#else
     constexpr int kLeafDen = SPH ? kSphParkDen : kTriParkDen;
+#endif
     extern __shared__ float4 lds[];
     __shared__ uint32_t seed_s[kFreeThreads];
     __shared__ float stash[kFsSlots * kFreeThreads];
@@ -487,7 +499,7 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
                 }
             }
             const int nfin = nlive - __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone || (live && idx < end)));
-            if (kFreeParkDen * nfin >= nlive) break;
+            if (kFreeParkDen * nfin >= kFreeParkNum * nlive) break;
         }
     }
 

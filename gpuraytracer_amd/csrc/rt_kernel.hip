@@ -415,7 +415,10 @@ __host__ __device__ constexpr bool halton_tables_on(int geo, bool small, uint32_
 }
 // box-cluster kernel: 7 waves/SIMD runs as fast as 8 and spills 6 VGPRs
 // instead of 30 (HBM traffic 146 MB instead of 19 GB per 1080p launch)
-constexpr int kMinWavesPerEuClu = 7;
+#ifndef RT_CLU_WAVES
+#define RT_CLU_WAVES 7
+#endif
+constexpr int kMinWavesPerEuClu = RT_CLU_WAVES;
 // L lanes per pixel (1, 4 or 16: more lanes when the launch has few pixels,
 // e.g. one GPU's share of a multi-GPU frame): lane `sub` of a pixel's
 // group traces samples n = r*L + sub of round r, and after every round the L
@@ -580,7 +583,11 @@ void path_trace_kernel(KParams P) {
             s.d = normalize((cu * sh + cv * th) - cw);
             s.o = ld_f3(P.cam_pos);
             s.thr = f3{1.0f, 1.0f, 1.0f};
+#ifndef RT_TIMING_NO_TRACE  // timing-only A/B (tools/ab_kernel.sh): camera, Halton jitter and sums alone
             trace_path<B, GEO, SPH, SMALL>(P, sv, s);                       // :47-102
+#else
+            s.acc = s.d;
+#endif
         }
         if (L == 1) {
             lum = lum + s.acc;                                   // :103

@@ -699,6 +699,31 @@ __device__ __forceinline__ void pair_test_rank(const float4* r, uint32_t k, f3 o
     }
 }
 
+#ifndef RT_CLU_HELP
+#define RT_CLU_HELP 0
+#endif
+// Position of the (r+1)-th set bit of a 64-bit mask (r < popcount).
+__device__ __forceinline__ uint32_t select_bit64(uint64_t m, uint32_t r) {
+    uint32_t pos = 0;
+    uint32_t lo = (uint32_t)m;
+    uint32_t c = (uint32_t)__builtin_popcount(lo);
+    if (r >= c) {
+        r -= c;
+        pos = 32;
+        lo = (uint32_t)(m >> 32);
+    }
+#pragma unroll
+    for (uint32_t w = 16; w >= 1; w >>= 1) {
+        c = (uint32_t)__builtin_popcount(lo & ((1u << w) - 1u));
+        if (r >= c) {
+            r -= c;
+            pos += w;
+            lo >>= w;
+        }
+    }
+    return pos;
+}
+
 // Closest hit / any hit over the pair records with box clusters: the
 // unclustered pairs by every lane (wave-uniform records, LDS broadcast), then
 // each lane's own candidate pairs (per-lane LDS reads).  For ANY, *best is
@@ -715,6 +740,66 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
     uint32_t cand = cluster_candidates<SEG>(sv, o, d, tmin, *best);
     RT_STAT(12, 1);
     RT_STAT(15, __popcll(__ballot(1)));
+#if RT_CLU_HELP
+    // A/B variant: candidate-round compaction.  In
+    // every round the lanes of the query with no candidate left help the
+    // lanes with two or more: a helper pulls its owner's ray, best and
+    // candidate mask (ds_bpermute), tests the owner's SECOND candidate while
+    // the owner tests its first, and the owner merges the two (t, id)-ranked
+    // results -- both started from the same (best, id), so their
+    // lexicographic minimum is the result of testing both in any order.
+    const uint32_t me = __lane_id();
+    for (;;) {
+        const bool want = cand != 0u && !(ANY && *id >= 0);
+        if (__builtin_amdgcn_ballot_w64(want) == 0) break;
+        const bool two = want && (cand & (cand - 1u)) != 0u;
+        const uint64_t m2 = __builtin_amdgcn_ballot_w64(two);
+        const uint64_t idle = __builtin_amdgcn_ballot_w64(!want);
+        const uint32_t n2 = (uint32_t)__popcll(m2), ni = (uint32_t)__popcll(idle);
+        uint32_t partner = me;
+        bool helped = false, helping = false;
+        if (two) {
+            const uint32_t q = (uint32_t)__popcll(m2 & ((1ull << me) - 1ull));
+            if (q < ni) {
+                partner = select_bit64(idle, q);
+                helped = true;
+            }
+        } else if (!want) {
+            const uint32_t r = (uint32_t)__popcll(idle & ((1ull << me) - 1ull));
+            if (r < n2) {
+                partner = select_bit64(m2, r);
+                helping = true;
+            }
+        }
+        const f3 po{__shfl(o.x, (int)partner), __shfl(o.y, (int)partner), __shfl(o.z, (int)partner)};
+        const f3 pd{__shfl(d.x, (int)partner), __shfl(d.y, (int)partner), __shfl(d.z, (int)partner)};
+        const uint32_t pc = (uint32_t)__shfl((int)cand, (int)partner);
+        float tb = __shfl(*best, (int)partner);
+        int tid = __shfl(*id, (int)partner);
+        RT_STAT(13, 1);
+        RT_STAT(14, __popcll(__ballot(want || helping)));
+        if (want || helping) {
+            const uint32_t k = (uint32_t)__builtin_ctz(helping ? (pc & (pc - 1u)) : pc);
+            pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, helping ? po : o, helping ? pd : d, tmin, &tb, &tid);
+        }
+        const float rb = __shfl(tb, (int)partner);
+        const int rid = __shfl(tid, (int)partner);
+        if (want) {
+            cand &= cand - 1u;
+            *best = tb;
+            *id = tid;
+            if (helped) {
+                cand &= cand - 1u;
+                if (ANY) {
+                    if (rid >= 0) *id = rid;
+                } else if (rb < *best || (rb == *best && rid < *id)) {
+                    *best = rb;
+                    *id = rid;
+                }
+            }
+        }
+    }
+#else
     while (cand != 0u && !(ANY && *id >= 0)) {
         RT_STAT(13, 1);
         RT_STAT(14, __popcll(__ballot(1)));
@@ -722,6 +807,7 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
         cand &= cand - 1u;
         pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, o, d, tmin, best, id);
     }
+#endif
 }
 
 // closest hit, accept_any_intersection(false) (raytrace.metal:48-49).
