@@ -124,28 +124,30 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     const bool lit = (GEO == kGeoTriBvh && b == 0) || contrib.x != 0.0f || contrib.y != 0.0f ||
                      contrib.z != 0.0f;
     if constexpr (STASH) {
-        // the sphere kernel parks contrib and the next direction in a per-lane
+        // the BVH kernels park contrib and the next direction in a per-lane
         // LDS stash across the shadow walk (read back through an opaque lane
         // index, so they are not kept in registers): at 64 VGPRs (8 waves/SIMD)
-        // they were 5 spilled VGPRs, 24 B of scratch per lane (round 4)
+        // they were 5-6 spilled VGPRs, 24-28 B of scratch per lane (round 4)
+        constexpr uint32_t SS = GEO == kGeoSphLds ? kSphBlockThreads : kBlockThreads;  // stash stride
         uint32_t t = threadIdx.x;
         asm volatile("" : "+v"(t));
         float* st = sv.xstash;
         st[t] = contrib.x;
-        st[kSphBlockThreads + t] = contrib.y;
-        st[2 * kSphBlockThreads + t] = contrib.z;
+        st[SS + t] = contrib.y;
+        st[2 * SS + t] = contrib.z;
         if (b + 1 < B) {
-            st[3 * kSphBlockThreads + t] = d2.x;
-            st[4 * kSphBlockThreads + t] = d2.y;
-            st[5 * kSphBlockThreads + t] = d2.z;
+            st[3 * SS + t] = d2.x;
+            st[4 * SS + t] = d2.y;
+            st[5 * SS + t] = d2.z;
         }
-        const bool occluded = lit && any_hit<GEO, SPH, false>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi);
+        const bool occluded =
+            lit && any_hit<GEO, SPH, b == 0 && !SPH>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi);  // :79-85
         uint32_t t2 = threadIdx.x;
         asm volatile("" : "+v"(t2));
-        if (lit && !occluded)                              // :79-89
-            s.acc = s.acc + f3{st[t2], st[kSphBlockThreads + t2], st[2 * kSphBlockThreads + t2]};
+        if (lit && !occluded)                              // :87-89
+            s.acc = s.acc + f3{st[t2], st[SS + t2], st[2 * SS + t2]};
         if (b + 1 < B) {
-            s.d = f3{st[3 * kSphBlockThreads + t2], st[4 * kSphBlockThreads + t2], st[5 * kSphBlockThreads + t2]};
+            s.d = f3{st[3 * SS + t2], st[4 * SS + t2], st[5 * SS + t2]};
             s.o = p;                                       // :99-100
         }
         return true;
@@ -166,7 +168,7 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     // Camera rays of an 8x8 tile are coherent: cull with their segment boxes.
     const int id = closest_hit<GEO, SPH, b == 0, (b == 0 ? 0 : 1)>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
     if (id < 0) return false;                               // :51-53
-    return shade<b, B, GEO, SPH, SMALL, false, GEO == kGeoSphLds>(P, sv, s, id, t);
+    return shade<b, B, GEO, SPH, SMALL, false, GEO == kGeoSphLds || GEO == kGeoTriBvh>(P, sv, s, id, t);
 }
 
 template <int b, int B, int GEO, bool SPH, bool SMALL>
@@ -477,6 +479,10 @@ void path_trace_kernel(KParams P) {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
     }
+    if (GEO == kGeoTriBvh) {  // per-lane stash of shade() across the shadow walks
+        __shared__ float tri_stash[GEO == kGeoTriBvh ? 6 * kBlockThreads : 1];
+        sv.xstash = tri_stash;
+    }
     sv.tnode = P.tri_nodes;
     sv.tsorted = P.tri_sorted;
     sv.tperm = P.tri_perm;
@@ -633,7 +639,11 @@ void path_trace_kernel(KParams P) {
         }
 #endif
     }
-    const uint32_t t = opaque_tid();
+    // the pixel of the epilogue, recomputed from an opaque copy of threadIdx.x
+    // in every kernel: otherwise the prologue's pixel offsets are kept (and
+    // spilled) across the whole sample loop
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
     if (L > 1) {
         if (t % L != 0) return;
         const uint32_t slot = t / L;
@@ -1012,6 +1022,7 @@ hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem m
     if (geo == kGeoFreeTri) return launch_free<3, kGeoTriBvh>(P, lds_total, stream);
     if (geo == kGeoSortSph) return launch_sorted_g<3, kGeoSphLds>(P, lds_total, stream);
     if (geo == kGeoSortTri) return launch_sorted_g<3, kGeoTriBvh>(P, lds_total, stream);
+    if (geo == kGeoTriBvh) return launch_g<3, kGeoTriBvh>(P, lds_total, stream);
     return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_total, stream)
                               : launch_g<3, kGeoSphLds>(P, lds_total, stream);
 #endif
