@@ -24,6 +24,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include <vector>
@@ -84,16 +85,15 @@ __global__ void tri_box_kernel(const float4* __restrict__ tri, uint32_t n, float
 // bins of one slot: count[3][kBins], lo[3][kBins][3], hi[3][kBins][3]
 constexpr uint32_t kSlotWords = 3 * kBins * 7;
 
-__global__ void bin_kernel(uint32_t n, const uint32_t* __restrict__ ids, const uint32_t* __restrict__ seg,
-                           const GNode* __restrict__ nodes, const float* __restrict__ bl,
-                           const float* __restrict__ bh, const float* __restrict__ cen,
-                           uint32_t* __restrict__ bins) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const GNode& N = nodes[seg[k]];
-    if (N.slot == kNoSlot) return;
-    const uint32_t t = ids[k];
-    uint32_t* B = bins + (size_t)N.slot * kSlotWords;
+// The same binning with the bins of a chunk of kBinChunk consecutive positions
+// privatised in LDS when the whole chunk belongs to one node (every chunk of
+// the top levels): the global atomics per bin drop from one per triangle to
+// one per chunk.  min / max / add are order-free: the same bins.
+constexpr uint32_t kBinThreads = 256, kBinChunk = 2048;
+
+__device__ __forceinline__ void bin_one(const GNode& N, uint32_t t, const float* __restrict__ bl,
+                                        const float* __restrict__ bh, const float* __restrict__ cen,
+                                        uint32_t* B) {
     for (int a = 0; a < 3; ++a) {
         const float clo = fdec(N.clo[a]), ext = fdec(N.chi[a]) - clo;
         if (!(ext > 0.0f)) continue;
@@ -101,11 +101,50 @@ __global__ void bin_kernel(uint32_t n, const uint32_t* __restrict__ ids, const u
         const int bi = min(kBins - 1, (int)((cen[3 * t + a] - clo) * scale));
         atomicAdd(&B[a * kBins + bi], 1u);
         uint32_t* lo = B + 3 * kBins + (a * kBins + bi) * 3;
-        uint32_t* hi = B + 3 * kBins + 9 * kBins + (a * kBins + bi) * 3;
+        uint32_t* hi = B + 12 * kBins + (a * kBins + bi) * 3;
         for (int q = 0; q < 3; ++q) {
             atomicMin(&lo[q], fenc(bl[3 * t + q]));
             atomicMax(&hi[q], fenc(bh[3 * t + q]));
         }
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void bin_chunk_kernel(uint32_t n, const uint32_t* __restrict__ ids,
+                                                                const uint32_t* __restrict__ seg,
+                                                                const GNode* __restrict__ nodes,
+                                                                const float* __restrict__ bl,
+                                                                const float* __restrict__ bh,
+                                                                const float* __restrict__ cen,
+                                                                uint32_t* __restrict__ bins) {
+    __shared__ uint32_t lb[kSlotWords];
+    const uint32_t base = blockIdx.x * kBinChunk;
+    const uint32_t end = min(base + kBinChunk, n);
+    const uint32_t v0 = seg[base];
+    if (v0 == seg[end - 1]) {  // one node (positions are grouped by node)
+        const GNode& N = nodes[v0];
+        if (N.slot == kNoSlot) return;
+        for (uint32_t w = threadIdx.x; w < kSlotWords; w += kBinThreads)
+            lb[w] = (w >= 3 * kBins && w < 12 * kBins) ? 0xFFFFFFFFu : 0u;
+        __syncthreads();
+        for (uint32_t k = base + threadIdx.x; k < end; k += kBinThreads) bin_one(N, ids[k], bl, bh, cen, lb);
+        __syncthreads();
+        uint32_t* B = bins + (size_t)N.slot * kSlotWords;
+        for (uint32_t w = threadIdx.x; w < kSlotWords; w += kBinThreads) {
+            const uint32_t v = lb[w];
+            if (w < 3 * kBins) {
+                if (v) atomicAdd(&B[w], v);
+            } else if (w < 12 * kBins) {
+                if (v != 0xFFFFFFFFu) atomicMin(&B[w], v);
+            } else if (v) {
+                atomicMax(&B[w], v);
+            }
+        }
+        return;
+    }
+    for (uint32_t k = base + threadIdx.x; k < end; k += kBinThreads) {
+        const GNode& N = nodes[seg[k]];
+        if (N.slot == kNoSlot) continue;
+        bin_one(N, ids[k], bl, bh, cen, bins + (size_t)N.slot * kSlotWords);
     }
 }
 
@@ -253,22 +292,10 @@ __global__ void make_children_kernel(uint32_t m, const uint32_t* __restrict__ ac
 }
 
 // Stable partition of the split nodes' positions into their children, and the
-// children's exact boxes and centroid boxes.
-__global__ void partition_kernel(uint32_t n, const uint32_t* __restrict__ ids, const uint32_t* __restrict__ seg,
-                                 const GNode* __restrict__ nodes_c, GNode* __restrict__ nodes,
-                                 const uint8_t* __restrict__ splitting, const uint32_t* __restrict__ lscan,
-                                 const uint32_t* __restrict__ lflag, const float* __restrict__ bl,
-                                 const float* __restrict__ bh, const float* __restrict__ cen,
-                                 uint32_t* __restrict__ ids2, uint32_t* __restrict__ seg2) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const uint32_t v = seg[k], t = ids[k];
-    if (!splitting[v]) {
-        ids2[k] = t;
-        seg2[k] = v;
-        return;
-    }
-    const GNode& N = nodes_c[v];
+// children's exact boxes and centroid boxes (atomic min / max, privatised in
+// LDS when a chunk of positions belongs to one node, as in bin_chunk_kernel).
+__device__ __forceinline__ uint32_t part_one(uint32_t k, uint32_t t, const GNode& N, const uint32_t* lscan,
+                                             const uint32_t* lflag, uint32_t* ids2, uint32_t* seg2) {
     const uint32_t e = N.begin + N.count - 1;
     const uint32_t nl = (lscan[e] + lflag[e]) - lscan[N.begin];
     const uint32_t before = lscan[k] - lscan[N.begin];  // left triangles before k in the node
@@ -282,12 +309,63 @@ __global__ void partition_kernel(uint32_t n, const uint32_t* __restrict__ ids, c
     }
     ids2[dst] = t;
     seg2[dst] = c;
-    GNode& C = nodes[c];
+    return c;
+}
+
+__device__ __forceinline__ void grow_bounds(uint32_t* w, uint32_t t, const float* bl, const float* bh,
+                                            const float* cen) {  // w: lo[3] hi[3] clo[3] chi[3]
     for (int a = 0; a < 3; ++a) {
-        atomicMin(&C.lo[a], fenc(bl[3 * t + a]));
-        atomicMax(&C.hi[a], fenc(bh[3 * t + a]));
-        atomicMin(&C.clo[a], fenc(cen[3 * t + a]));
-        atomicMax(&C.chi[a], fenc(cen[3 * t + a]));
+        atomicMin(&w[a], fenc(bl[3 * t + a]));
+        atomicMax(&w[3 + a], fenc(bh[3 * t + a]));
+        atomicMin(&w[6 + a], fenc(cen[3 * t + a]));
+        atomicMax(&w[9 + a], fenc(cen[3 * t + a]));
+    }
+}
+
+__global__ __launch_bounds__(kBinThreads) void partition_kernel(
+    uint32_t n, const uint32_t* __restrict__ ids, const uint32_t* __restrict__ seg, GNode* __restrict__ nodes,
+    const uint8_t* __restrict__ splitting, const uint32_t* __restrict__ lscan, const uint32_t* __restrict__ lflag,
+    const float* __restrict__ bl, const float* __restrict__ bh, const float* __restrict__ cen,
+    uint32_t* __restrict__ ids2, uint32_t* __restrict__ seg2) {
+    static_assert(offsetof(GNode, hi) == offsetof(GNode, lo) + 12 && offsetof(GNode, clo) == offsetof(GNode, lo) + 24 &&
+                      offsetof(GNode, chi) == offsetof(GNode, lo) + 36,
+                  "GNode bounds are 12 consecutive words");
+    __shared__ uint32_t cb[2][12];
+    const uint32_t base = blockIdx.x * kBinChunk;
+    const uint32_t end = min(base + kBinChunk, n);
+    const uint32_t v0 = seg[base];
+    if (v0 == seg[end - 1] && splitting[v0]) {  // one node being split
+        const GNode N = nodes[v0];
+        if (threadIdx.x < 24) cb[threadIdx.x / 12][threadIdx.x % 12] = (threadIdx.x % 6 < 3) ? 0xFFFFFFFFu : 0u;
+        __syncthreads();
+        for (uint32_t k = base + threadIdx.x; k < end; k += kBinThreads) {
+            const uint32_t t = ids[k];
+            const uint32_t c = part_one(k, t, N, lscan, lflag, ids2, seg2);
+            grow_bounds(cb[c == N.left ? 0 : 1], t, bl, bh, cen);
+        }
+        __syncthreads();
+        if (threadIdx.x < 24) {
+            const uint32_t side = threadIdx.x / 12, w = threadIdx.x % 12;
+            uint32_t* dst = nodes[side ? N.right : N.left].lo + w;
+            const uint32_t v = cb[side][w];
+            if (w % 6 < 3) {
+                if (v != 0xFFFFFFFFu) atomicMin(dst, v);
+            } else if (v) {
+                atomicMax(dst, v);
+            }
+        }
+        return;
+    }
+    for (uint32_t k = base + threadIdx.x; k < end; k += kBinThreads) {
+        const uint32_t v = seg[k], t = ids[k];
+        if (!splitting[v]) {
+            ids2[k] = t;
+            seg2[k] = v;
+            continue;
+        }
+        const GNode& N = nodes[v];
+        const uint32_t c = part_one(k, t, N, lscan, lflag, ids2, seg2);
+        grow_bounds(nodes[c].lo, t, bl, bh, cen);
     }
 }
 
@@ -483,7 +561,8 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
             // bins: counts 0, lo = +inf (0xFFFFFFFF), hi = -inf (0)
             hipLaunchKernelGGL(clear_bins_kernel, grid1(m * kSlotWords), dim3(256), 0, s, bins, m);
             hipLaunchKernelGGL(assign_slots_kernel, grid1(m), dim3(256), 0, s, m, active, nodes);
-            hipLaunchKernelGGL(bin_kernel, grid1(n), dim3(256), 0, s, n, ids, seg, nodes, bl, bh, cen, bins);
+            hipLaunchKernelGGL(bin_chunk_kernel, dim3((n + kBinChunk - 1) / kBinChunk), dim3(kBinThreads), 0, s,
+                               n, ids, seg, nodes, bl, bh, cen, bins);
             hipLaunchKernelGGL(split_kernel, grid1(m, 64), dim3(64), 0, s, m, active, nodes, bins, leaf_max,
                                trav_cost, margin, split_flag);
             if ((e = scan_u32(split_flag, split_rank, m, tiles, s))) break;
@@ -500,8 +579,8 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
             const uint32_t child_off = list_off + m;
             hipLaunchKernelGGL(make_children_kernel, grid1(m), dim3(256), 0, s, m, active, nodes, split_flag,
                                split_rank, next_free, lscan, lflag, lists + child_off);
-            hipLaunchKernelGGL(partition_kernel, grid1(n), dim3(256), 0, s, n, ids, seg, nodes, nodes, splitting,
-                               lscan, lflag, bl, bh, cen, ids2, seg2);
+            hipLaunchKernelGGL(partition_kernel, dim3((n + kBinChunk - 1) / kBinChunk), dim3(kBinThreads), 0, s,
+                               n, ids, seg, nodes, splitting, lscan, lflag, bl, bh, cen, ids2, seg2);
             hipLaunchKernelGGL(mark_kernel, grid1(m), dim3(256), 0, s, m, active, (const uint32_t*)nullptr, splitting);
             if ((e = hipGetLastError())) break;
             std::swap(ids, ids2);

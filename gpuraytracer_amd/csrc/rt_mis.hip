@@ -378,7 +378,10 @@ constexpr uint32_t kMisRowPixels = 64u / kMisLanes;
 // 7 waves/SIMD: 72 VGPRs without scratch since the primary hit, the pixel sum,
 // dl/dc and the running strategy sum wait in the per-lane LDS stash (round 2:
 // 120 VGPRs at 4 waves; 6 waves then spilled 54 VGPRs).  DESIGN.md §5
-constexpr int kMisWavesPerEu = 7;
+#ifndef RT_MIS_WAVES
+#define RT_MIS_WAVES 7
+#endif
+constexpr int kMisWavesPerEu = RT_MIS_WAVES;
 // FREEP: the scene has pairs in no box cluster (P.pair_free != 0).  The
 // reference scene has none; with FREEP false their loop is compiled out, which
 // also drops the one VGPR its loop-invariant test occupied (8 B of scratch at

@@ -57,6 +57,7 @@ def test_create_rejects_bad_descriptions_without_a_device():
 
 
 def test_null_context_calls_return_status():
+    assert g.lib.rt_build_info(None, None) == 1
     assert g.lib.rt_render(None, None, None) == 1
     assert g.lib.rt_fill_seeds(None, 0) == 1
     assert g.lib.rt_destroy(None) == 0

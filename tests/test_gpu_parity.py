@@ -450,6 +450,31 @@ def test_triangle_bvh_gpu_build_bit_exact(n, dup, build):
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"soup{n}")
 
 
+@pytest.mark.parametrize("build", ["gpusah", "host"])
+def test_triangle_bvh_coincident_centroids(build):
+    """600 copies of one small triangle (every centroid in one point: the SAH
+    builds split such a node by index) plus the room: bit-exact, ties to the
+    lower id, and the GPU build reports 2n - 1 nodes."""
+    base = Scene.cornell_box(40, 24)
+    n = 36 + 600
+    mats = (MaterialGPU * n)()
+    verts = (float3 * (3 * n))()
+    ctypes_memmove(mats, base.materials, 36 * 48)
+    ctypes_memmove(verts, base.vertices, 108 * 16)
+    for k in range(36, n):
+        for j, p in enumerate(((0.1, -0.5, 0.2), (0.35, -0.45, 0.25), (0.15, -0.2, 0.1))):
+            verts[3 * k + j].x, verts[3 * k + j].y, verts[3 * k + j].z = p
+        m = mats[k]
+        m.diffuse.x, m.diffuse.y, m.diffuse.z, m.diffuse.w = 0.2 + 0.6 * (k % 7) / 7.0, 0.5, 0.5, 1.0
+    s = Scene(base.camera, mats, verts, base.light)
+    sd = seed_splitmix(40, 24)
+    with Renderer(s, seeds=sd, options=Options(tri_build=build)) as r:
+        out = r.render(RenderParams(spp=3, bounces=3))
+        info = r.build_info()
+    assert info["tri_bvh_nodes"] == 2 * n - 1, info
+    assert_parity(out, oracle_lib.render(s, sd, 3, 3), f"coincident {build}")
+
+
 def test_triangle_bvh_forced_on_cornell_and_mis(monkeypatch):
     s = Scene.cornell_box(64, 48)
     sd = seed_splitmix(64, 48)

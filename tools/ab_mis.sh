@@ -10,5 +10,5 @@ SRC=${MIS_SRC:-$R/gpuraytracer_amd/csrc/rt_mis.hip}
     -I"$R/gpuraytracer_amd/csrc" --offload-arch=gfx950 -fno-slp-vectorize "$@" -c "$SRC" \
     -o "$R/build_a/rt_mis_$N.o"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$R/abvar/librtpt_$N.so" "$R/build/rt_kernel.o" \
-    "$R/build_a/rt_mis_$N.o" "$R/build/rt_lbvh.o" "$R/build/rt_api.o" "$R/build/rt_scene.o" \
+    "$R/build_a/rt_mis_$N.o" "$R/build/rt_lbvh.o" "$R/build/rt_gsah.o" "$R/build/rt_api.o" "$R/build/rt_scene.o" \
     "$R/build/rt_image.o" -L/opt/rocm/lib -lrccl
