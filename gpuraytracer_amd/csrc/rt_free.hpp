@@ -1,5 +1,9 @@
 // rt_free.hpp — the free-running path kernel for BVH scenes (sphere scenes
 // of config 4, triangle meshes): included by rt_kernel.hip inside namespace rt.
+// Opt-in (rt_create_options.walk_scheduler = RT_WALK_FREE): measured slower
+// than the lockstep kernels (config 4: 2,808 vs 3,531 Msamples/s; 100k
+// triangles 705 vs 844; profiles/r5/ab_results.md), kept because it is
+// bit-exact and documents the measurement.
 //
 // The lockstep kernel (path_trace_kernel) runs each bounce's queries for all
 // 64 lanes of a wave together, so a wave walks as long as its LONGEST walk:
@@ -8,15 +12,17 @@
 // its spp samples one after another (raytrace.metal:34-104) as its own state
 // machine; the wave never waits for one query to finish everywhere:
 //   * walk phase: every lane whose query is walking takes BVH steps; a lane
-//     whose walk ends (or meets a leaf to test) parks;
-//   * service phase, once at least half the live lanes are parked
-//     (kFreeParkDen): the parked leaves are tested (sphere roots, leaf
-//     triangles), and every lane whose walk ended runs the shading of
-//     raytrace.metal:55-101 up to its NEXT query (shadow any-hit, the next
-//     bounce's closest hit, or the next sample's camera ray), then walks again.
-// Walks therefore run at 50-100 % of the lanes, and the shading runs for half
-// a wave or more at a time (after Aila & Laine's persistent threads with
-// ray regeneration, here inside one path tracer's state machine).
+//     that meets a leaf worth testing parks it (tested for all parked lanes
+//     together once they are 1/kLeafDen of the walking lanes), a lane whose
+//     walk ended waits;
+//   * service phase, once at least half the live lanes have finished their
+//     query: every such lane runs the shading of raytrace.metal:55-101 up to
+//     its NEXT query (shadow any-hit, the next bounce's closest hit, or the
+//     next sample's camera ray), then walks again.
+// (After Aila & Laine's persistent threads with ray regeneration, inside one
+// path tracer's state machine.)  It loses because the lanes of a wave are at
+// different queries of different pixels: a node load touches up to 64 cache
+// lines where the lockstep kernel's 16-lanes-per-pixel waves share most.
 //
 // Bit parity: a lane computes exactly the operations of the lockstep kernel
 // for its pixel, in the same order -- the same Halton dimensions (the bounce

@@ -161,6 +161,13 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     return true;
 }
 
+// The triangle-BVH kernel runs WITHOUT the LDS stash of shade(): with it the
+// kernel has no scratch (63 VGPRs) but ran 778 vs 846 Msamples/s on 100k
+// triangles (round 5, profiles/r5/ab_results.md); without it 18 VGPRs spill
+// (16 B of scratch per lane, L2-resident)
+#ifndef RT_TRI_STASH
+#define RT_TRI_STASH 0
+#endif
 // One bounce b of raytrace.metal:47-101.  Returns false when the path ends.
 template <int b, int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, PathState& s) {
@@ -168,7 +175,8 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     // Camera rays of an 8x8 tile are coherent: cull with their segment boxes.
     const int id = closest_hit<GEO, SPH, b == 0, (b == 0 ? 0 : 1)>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
     if (id < 0) return false;                               // :51-53
-    return shade<b, B, GEO, SPH, SMALL, false, GEO == kGeoSphLds || GEO == kGeoTriBvh>(P, sv, s, id, t);
+    return shade<b, B, GEO, SPH, SMALL, false, GEO == kGeoSphLds || (RT_TRI_STASH && GEO == kGeoTriBvh)>(P, sv, s, id,
+                                                                                                 t);
 }
 
 template <int b, int B, int GEO, bool SPH, bool SMALL>
@@ -479,8 +487,8 @@ void path_trace_kernel(KParams P) {
         sv.tri = P.tri_isect;
         sv.pair = nullptr;
     }
-    if (GEO == kGeoTriBvh) {  // per-lane stash of shade() across the shadow walks
-        __shared__ float tri_stash[GEO == kGeoTriBvh ? 6 * kBlockThreads : 1];
+    if (GEO == kGeoTriBvh && RT_TRI_STASH) {  // per-lane stash of shade() across the shadow walks
+        __shared__ float tri_stash[GEO == kGeoTriBvh && RT_TRI_STASH ? 6 * kBlockThreads : 1];
         sv.xstash = tri_stash;
     }
     sv.tnode = P.tri_nodes;

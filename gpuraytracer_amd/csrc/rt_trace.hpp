@@ -774,12 +774,14 @@ __device__ __forceinline__ void cluster_query(const SceneView& sv, f3 o, f3 d, f
         const f3 po{__shfl(o.x, (int)partner), __shfl(o.y, (int)partner), __shfl(o.z, (int)partner)};
         const f3 pd{__shfl(d.x, (int)partner), __shfl(d.y, (int)partner), __shfl(d.z, (int)partner)};
         const uint32_t pc = (uint32_t)__shfl((int)cand, (int)partner);
-        float tb = __shfl(*best, (int)partner);
-        int tid = __shfl(*id, (int)partner);
+        const float ob = __shfl(*best, (int)partner);
+        const int oid = __shfl(*id, (int)partner);
+        float tb = helping ? ob : *best;  // a helper starts from its owner's (best, id)
+        int tid = helping ? oid : *id;
         RT_STAT(13, 1);
         RT_STAT(14, __popcll(__ballot(want || helping)));
         if (want || helping) {
-            const uint32_t k = (uint32_t)__builtin_ctz(helping ? (pc & (pc - 1u)) : pc);
+            const uint32_t k = (uint32_t)__builtin_ctz(helping ? (pc & (pc - 1u)) : cand);
             pair_test_rank<ANY>(sv.pair + kPairF4 * k, k, helping ? po : o, helping ? pd : d, tmin, &tb, &tid);
         }
         const float rb = __shfl(tb, (int)partner);
