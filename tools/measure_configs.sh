@@ -23,5 +23,6 @@ run c4_spheres1000 180 python bench.py --scene spheres --steps 3 --warmup 1 --cp
 run c5_share_8192sq_512spp_progressive64 240 python bench.py --width 8192 --height 8192 --spp 512 --batch-spp 64 --steps 2 --warmup 1 --cpu-baseline off
 run triangles10k 180 python bench.py --scene triangles --triangles 10000 --spp 64 --steps 2 --warmup 1 --cpu-baseline off
 run triangles100k 180 python bench.py --scene triangles --triangles 100000 --spp 64 --steps 2 --warmup 1 --cpu-baseline off
+run triangles1m 240 python bench.py --scene triangles --triangles 1000000 --spp 16 --steps 2 --warmup 1 --cpu-baseline off
 run multi_gpu_shares 180 python tools/bench_share.py
 run mis_800x600_c6_m300 240 python tools/bench_mis.py
