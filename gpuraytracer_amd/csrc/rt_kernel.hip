@@ -106,7 +106,13 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
     }
     if (FUSE && b + 1 < B) {
-        const FusedHit h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
+        FusedHit h;
+        if constexpr (GEO == kGeoTriBvh) {
+            const bool lit = contrib.x != 0.0f || contrib.y != 0.0f || contrib.z != 0.0f;
+            h = tri_walk_dual(sv, p, L, dist - 1e-3f, lit, d2);
+        } else {
+            h = fused_shadow_closest(sv, p, L, dist - 1e-3f, seg_lo, seg_hi, d2);
+        }
         if (!h.occluded) s.acc = s.acc + contrib;          // :79-89
         s.d = d2;
         s.o = p;                                           // :99-100
@@ -229,8 +235,43 @@ struct FusedChain<B, B, GEO, SMALL> {
 // closest hit of bounce b + 1 (fused_shadow_closest).  The box-cluster kernel
 // does not: its fused candidate rounds measured 5 % slower on Cornell 1080p
 // (DESIGN.md §5).
+// Triangle-BVH chain with the dual walks (RT_TRI_DUAL): bounce 0 as usual
+// (packet walks), then for b >= 1 the shadow query of b and the closest hit of
+// b + 1 in one tri_walk_dual loop.
+template <int b, int B, bool SMALL>
+struct TriDualChain {
+    __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv, PathState& s, int id,
+                                               float t) {
+        if constexpr (b + 1 < B) {
+            int nid = -1;
+            float nt = 0.0f;
+            if (!shade<b, B, kGeoTriBvh, false, SMALL, true>(P, sv, s, id, t, &nid, &nt)) return;
+            if (nid >= 0) TriDualChain<b + 1, B, SMALL>::run(P, sv, s, nid, nt);
+        } else {
+            (void)shade<b, B, kGeoTriBvh, false, SMALL>(P, sv, s, id, t);
+        }
+    }
+};
+template <int B, bool SMALL>
+struct TriDualChain<B, B, SMALL> {
+    __device__ __forceinline__ static void run(const KParams&, const SceneView&, PathState&, int, float) {}
+};
+
+#ifndef RT_TRI_DUAL
+#define RT_TRI_DUAL 0
+#endif
+
 template <int B, int GEO, bool SPH, bool SMALL>
 __device__ __forceinline__ void trace_path(const KParams& P, const SceneView& sv, PathState& s) {
+    if constexpr (RT_TRI_DUAL && GEO == kGeoTriBvh && !SPH && B > 1) {
+        float t = 1000.0f;                                  // sampling.metal:155
+        const int id = closest_hit<GEO, false, true, 0>(sv, s.o, s.d, 0.001f, &t);
+        if (id < 0 || !shade<0, B, GEO, false, SMALL>(P, sv, s, id, t)) return;
+        float t1 = 1000.0f;
+        const int id1 = closest_hit<GEO, false, false, 1>(sv, s.o, s.d, 0.001f, &t1);
+        if (id1 >= 0) TriDualChain<1, B, SMALL>::run(P, sv, s, id1, t1);
+        return;
+    }
     if (geo_pairs(GEO) && !SPH && B > 1) {
         float t = 1000.0f;                                  // sampling.metal:155
         const int id = closest_hit<GEO, false, true, 0>(sv, s.o, s.d, 0.001f, &t);
@@ -444,9 +485,13 @@ constexpr uint32_t waves_per_row(int geo) { return block_threads(geo) >= 128 ? 2
 constexpr uint32_t waves_per_col(int geo) { return block_threads(geo) / 64u / waves_per_row(geo); }
 
 template <int B, int GEO, bool SPH, bool SMALL, int L = 1>
+#ifndef RT_TRI_WAVES
+#define RT_TRI_WAVES 8
+#endif
 __global__ __launch_bounds__(block_threads(GEO),
                              SPH ? kMinWavesPerEuSph
-                                 : (GEO == kGeoPairClu ? kMinWavesPerEuClu : kMinWavesPerEu))
+                                 : (GEO == kGeoPairClu ? kMinWavesPerEuClu
+                                                       : (GEO == kGeoTriBvh ? RT_TRI_WAVES : kMinWavesPerEu)))
 void path_trace_kernel(KParams P) {
     constexpr uint32_t NT = block_threads(GEO), WR = waves_per_row(GEO), WC = waves_per_col(GEO);
     extern __shared__ float4 lds[];

@@ -1026,5 +1026,73 @@ __device__ __forceinline__ FusedHit fused_shadow_closest(const SceneView& sv, f3
     return h;
 }
 
+// Dual walk of the triangle BVH (A/B variant RT_TRI_DUAL, round 5): the
+// shadow any-hit of bounce b (from p toward the light sample, A) and the
+// closest hit of bounce b + 1 (from the same p along the next direction, B)
+// are independent, so one loop walks both per lane, loading both rays' next
+// entries before testing either: two dependent-load chains in flight per lane
+// instead of one (the 100k-triangle walks wait on memory, not on issue).
+// Each ray visits the same entries in the same order as tri_cbvh_walk and is
+// ranked the same way: the same results.
+__device__ __forceinline__ FusedHit tri_walk_dual(const SceneView& sv, f3 p, f3 dA, float tmaxA, bool litA, f3 dB) {
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const uint4* __restrict__ cn = sv.tnode;
+    const uint32_t nN = sv.nTN;
+    const RayBox ra = ray_box(p, dA), rb = ray_box(p, dB);
+    uint32_t ia = octant(dA) * nN;
+    const uint32_t ea = ia + nN;
+    if (!litA) ia = ea;
+    uint32_t ib = octant(dB) * nN;
+    const uint32_t eb = ib + nN;
+    uint32_t la = kNone, lb = kNone;
+    FusedHit h{false, -1, 1000.0f};  // max_distance (sampling.metal:155)
+    for (;;) {
+        for (;;) {
+            const bool aa = ia < ea && la == kNone, ab = ib < eb && lb == kNone;
+            if (__builtin_amdgcn_ballot_w64(aa || ab) == 0) break;
+            // both entries requested before either is tested (clamped indices:
+            // a finished ray re-reads an entry of its own layout, unused)
+            const uint4 na = cn[aa ? ia : ea - 1u];
+            const uint4 nb = cn[ab ? ib : eb - 1u];
+            if (aa) {
+                const bool inner = (na.w & 0x80000000u) != 0u;
+                if (!lds_node_hit(na, ra, 0.0f, tmaxA)) {
+                    ia = inner ? (na.w & 0x7FFFFFFFu) : ia + 1;
+                } else {
+                    if (!inner) la = na.w;
+                    ia = ia + 1;
+                }
+            }
+            if (ab) {
+                const bool inner = (nb.w & 0x80000000u) != 0u;
+                if (!lds_node_hit(nb, rb, 0.001f, h.t)) {
+                    ib = inner ? (nb.w & 0x7FFFFFFFu) : ib + 1;
+                } else {
+                    if (!inner) lb = nb.w;
+                    ib = ib + 1;
+                }
+            }
+            const int parked = __popcll(__builtin_amdgcn_ballot_w64(la != kNone)) +
+                               __popcll(__builtin_amdgcn_ballot_w64(lb != kNone));
+            const int live = __popcll(__builtin_amdgcn_ballot_w64(ia < ea || la != kNone)) +
+                             __popcll(__builtin_amdgcn_ballot_w64(ib < eb || lb != kNone));
+            if (kTriParkDen * parked >= live) break;
+        }
+        if (__builtin_amdgcn_ballot_w64(la != kNone || lb != kNone) == 0) break;
+        if (la != kNone) {
+            if (tri_leaf_any(sv.tsorted, la, p, dA, 0.0f, tmaxA)) {
+                h.occluded = true;
+                ia = ea;
+            }
+            la = kNone;
+        }
+        if (lb != kNone) {
+            tri_leaf_closest(sv.tsorted, sv.tperm, lb, p, dB, 0.001f, h.t, h.id);
+            lb = kNone;
+        }
+    }
+    return h;
+}
+
 }  // namespace
 }  // namespace rt
