@@ -467,7 +467,7 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
                 } else {
                     const uint4 e = sv.tnode[idx];
                     const bool inner = (e.w & 0x80000000u) != 0u;
-                    if (!lds_node_hit(e, rb, tmin, best)) {
+                    if (!lds_node_hit_nf(e, rb, tmin, best)) {
                         idx = inner ? (e.w & 0x7FFFFFFFu) : idx + 1;
                     } else {
                         if (!inner) leaf = e.w;

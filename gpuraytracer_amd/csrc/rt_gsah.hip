@@ -472,11 +472,20 @@ __global__ void emit_kernel(uint32_t total, const GNode* __restrict__ nodes, con
     const float lx = fdec(N.lo[0]) - margin, ly = fdec(N.lo[1]) - margin, lz = fdec(N.lo[2]) - margin;
     const float hx = fdec(N.hi[0]) + margin, hy = fdec(N.hi[1]) + margin, hz = fdec(N.hi[2]) + margin;
     // the box in fp16 rounded outward (a superset of the padded box)
-    const uint32_t h0 = __half_as_ushort(__float2half_rd(lx)), h1 = __half_as_ushort(__float2half_rd(ly));
-    const uint32_t h2 = __half_as_ushort(__float2half_rd(lz)), h3 = __half_as_ushort(__float2half_ru(hx));
-    const uint32_t h4 = __half_as_ushort(__float2half_ru(hy)), h5 = __half_as_ushort(__float2half_ru(hz));
+    uint32_t h[6] = {__half_as_ushort(__float2half_rd(lx)), __half_as_ushort(__float2half_rd(ly)),
+                     __half_as_ushort(__float2half_rd(lz)), __half_as_ushort(__float2half_ru(hx)),
+                     __half_as_ushort(__float2half_ru(hy)), __half_as_ushort(__float2half_ru(hz))};
+    // near/far: in the layout of octant `oct` the plane a ray of that octant
+    // enters through takes the lo slot (rt_trace.hpp lds_node_hit_nf)
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        if ((oct >> a) & 1u) {
+            const uint32_t x = h[a];
+            h[a] = h[3 + a];
+            h[3 + a] = x;
+        }
     const uint32_t w = N.leaf ? (N.begin | (N.count - 1u) << 24) : ((oct * total + p + size[v]) | 0x80000000u);
-    out[(size_t)oct * total + p] = make_uint4(h0 | (h1 << 16), h2 | (h3 << 16), h4 | (h5 << 16), w);
+    out[(size_t)oct * total + p] = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), w);
 }
 
 __global__ void gather_sorted_kernel(const float4* __restrict__ tri, const uint32_t* __restrict__ ids, uint32_t n,

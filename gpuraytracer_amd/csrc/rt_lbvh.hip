@@ -160,11 +160,19 @@ __global__ void layout_kernel(uint32_t n, const uint32_t* __restrict__ child,
     // node (an entry index over all 8 layouts) or the leaf's triangle index in
     // leaf order (a leaf's escape is the next entry)
     uint4* cn = nodes + (size_t)oct * total + idx;
-    const uint32_t h0 = __half_as_ushort(__float2half_rd(b0.x)), h1 = __half_as_ushort(__float2half_rd(b0.y));
-    const uint32_t h2 = __half_as_ushort(__float2half_rd(b0.z)), h3 = __half_as_ushort(__float2half_ru(b1.x));
-    const uint32_t h4 = __half_as_ushort(__float2half_ru(b1.y)), h5 = __half_as_ushort(__float2half_ru(b1.z));
+    uint32_t h[6] = {__half_as_ushort(__float2half_rd(b0.x)), __half_as_ushort(__float2half_rd(b0.y)),
+                     __half_as_ushort(__float2half_rd(b0.z)), __half_as_ushort(__float2half_ru(b1.x)),
+                     __half_as_ushort(__float2half_ru(b1.y)), __half_as_ushort(__float2half_ru(b1.z))};
+    // near/far: the plane a ray of octant `oct` enters through takes the lo slot
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        if ((oct >> a) & 1u) {
+            const uint32_t x = h[a];
+            h[a] = h[3 + a];
+            h[3 + a] = x;
+        }
     const uint32_t w = (v >= n - 1) ? (v - (n - 1)) : ((oct * total + escape) | 0x80000000u);
-    *cn = make_uint4(h0 | (h1 << 16), h2 | (h3 << 16), h4 | (h5 << 16), w);
+    *cn = make_uint4(h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), w);
 }
 
 __global__ void gather_kernel(const float4* __restrict__ tri, const uint32_t* __restrict__ ids,

@@ -706,6 +706,9 @@ bool build_tri_sah(const std::vector<TriIsect>& tri, float margin, std::vector<u
             for (int a = 0; a < 3; ++a) {
                 h[a] = half_dir(N.lo[a], -1);
                 h[3 + a] = half_dir(N.hi[a], +1);
+                // near/far boxes as in the sphere layouts: the plane a ray of this
+                // octant enters through takes the lo slot (rt_trace.hpp lds_node_hit_nf)
+                if ((oct >> a) & 1u) std::swap(h[a], h[3 + a]);
             }
             uint32_t* w = L + 4 * (size_t)idx;
             w[0] = h[0] | (uint32_t)h[1] << 16;

@@ -419,9 +419,12 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
 }
 
 // Triangle-BVH walks over the compact entries (rt_scene.cpp build_tri_sah or
-// rt_lbvh.hip: 16 B per node, fp16 boxes rounded outward, one layout per
-// direction octant, near child first): stackless depth-first walks with
-// conservative boxes and (t, id) ranking.
+// rt_lbvh.hip, rt_gsah.hip: 16 B per node, fp16 near/far boxes rounded
+// outward, one layout per direction octant, near child first): stackless
+// depth-first walks with conservative boxes and (t, id) ranking (DESIGN.md
+// §3.10).  A per-lane walk is in its own octant's layout and tests near/far
+// (lds_node_hit_nf); the wave-packet walks below use the lane-0 layout for
+// every lane and the min/max test, which does not depend on the slot order.
 
 // A leaf of the triangle BVH: up to 128 consecutive triangles in leaf order,
 // word = first | (count - 1) << 24 (build_tri_sah makes leaves of up to
@@ -527,7 +530,7 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
             if (adv) {
                 const uint4 e = cn[idx];
                 const bool inner = (e.w & 0x80000000u) != 0u;
-                if (!lds_node_hit(e, rb, tmin, best)) {
+                if (!lds_node_hit_nf(e, rb, tmin, best)) {
                     idx = inner ? (e.w & 0x7FFFFFFFu) : idx + 1;
                 } else {
                     if (!inner) leaf = e.w;
@@ -1056,7 +1059,7 @@ __device__ __forceinline__ FusedHit tri_walk_dual(const SceneView& sv, f3 p, f3 
             const uint4 nb = cn[ab ? ib : eb - 1u];
             if (aa) {
                 const bool inner = (na.w & 0x80000000u) != 0u;
-                if (!lds_node_hit(na, ra, 0.0f, tmaxA)) {
+                if (!lds_node_hit_nf(na, ra, 0.0f, tmaxA)) {
                     ia = inner ? (na.w & 0x7FFFFFFFu) : ia + 1;
                 } else {
                     if (!inner) la = na.w;
@@ -1065,7 +1068,7 @@ __device__ __forceinline__ FusedHit tri_walk_dual(const SceneView& sv, f3 p, f3 
             }
             if (ab) {
                 const bool inner = (nb.w & 0x80000000u) != 0u;
-                if (!lds_node_hit(nb, rb, 0.001f, h.t)) {
+                if (!lds_node_hit_nf(nb, rb, 0.001f, h.t)) {
                     ib = inner ? (nb.w & 0x7FFFFFFFu) : ib + 1;
                 } else {
                     if (!inner) lb = nb.w;

@@ -26,13 +26,16 @@ static float half_to_float(uint16_t h) {
 
 struct Box { double lo[3], hi[3]; };
 
-static Box entry_box(const uint32_t* w) {
+// near/far entries: in the layout of octant `oct` the lo slot of axis a holds
+// the plane a ray of that octant enters through (hi when bit a is set)
+static Box entry_box(const uint32_t* w, uint32_t oct) {
     const uint16_t h[6] = {(uint16_t)(w[0] & 0xFFFF), (uint16_t)(w[0] >> 16), (uint16_t)(w[1] & 0xFFFF),
                            (uint16_t)(w[1] >> 16), (uint16_t)(w[2] & 0xFFFF), (uint16_t)(w[2] >> 16)};
     Box b;
     for (int a = 0; a < 3; ++a) {
-        b.lo[a] = half_to_float(h[a]);
-        b.hi[a] = half_to_float(h[3 + a]);
+        const bool neg = (oct >> a) & 1u;
+        b.lo[a] = half_to_float(h[neg ? 3 + a : a]);
+        b.hi[a] = half_to_float(h[neg ? a : 3 + a]);
     }
     return b;
 }
@@ -117,13 +120,14 @@ int main(int argc, char** argv) {
         std::vector<int> cover(n, 0);
         for (uint32_t i = 0; i < total; ++i) {
             const uint32_t* w = L + 4 * (size_t)i;
-            const Box b = entry_box(w);
+            const Box b = entry_box(w, oct);
+            for (int a = 0; a < 3; ++a) CHECK(b.lo[a] <= b.hi[a], "oct %u entry %u: near/far order", oct, i);
             if (w[3] & 0x80000000u) {
                 const uint32_t esc = (w[3] & 0x7FFFFFFFu) - oct * total;
                 CHECK(esc > i + 1 && esc <= total, "oct %u entry %u: escape %u", oct, i, esc);
                 // the box holds every entry of its subtree [i+1, esc)
                 for (uint32_t j = i + 1; j < esc; ++j) {
-                    const Box c = entry_box(L + 4 * (size_t)j);
+                    const Box c = entry_box(L + 4 * (size_t)j, oct);
                     for (int a = 0; a < 3; ++a)
                         CHECK(b.lo[a] <= c.lo[a] && c.hi[a] <= b.hi[a], "oct %u: entry %u box not inside %u", oct, j, i);
                 }
@@ -162,7 +166,7 @@ int main(int argc, char** argv) {
         for (uint32_t i = 0; i < total;) {
             const uint32_t* w = L + 4 * (size_t)i;
             const bool inner = (w[3] & 0x80000000u) != 0;
-            if (!box_hit(entry_box(w), o, d, wt)) {
+            if (!box_hit(entry_box(w, oct), o, d, wt)) {
                 i = inner ? (w[3] & 0x7FFFFFFFu) - oct * total : i + 1;
                 continue;
             }
