@@ -190,7 +190,7 @@ struct BounceChain {
     __device__ __forceinline__ static void run(const KParams& P, const SceneView& sv,
                                                PathState& s) {
 #ifdef RT_STATS
-        if constexpr (!SPH) {  // slots 16-31 are the sphere walks' in sphere scenes
+        if constexpr (!SPH && GEO != kGeoTriBvh) {  // slots 16-31: the per-lane BVH walks' otherwise
             // lane-slot accounting of the triangle kernels (tools/kernel_stats.py):
             // shader-clock cycles of this bounce per wave, and the same weighted
             // by the lanes whose path is still alive when it starts (16+b, 20+b)

@@ -466,7 +466,9 @@ __device__ __forceinline__ void tri_cbvh_closest_packet(const uint4* __restrict_
     const RayBox rb = ray_box(o, d);
     uint32_t idx = wave_uniform(octant(d)) * nN;
     const uint32_t end = idx + nN;
+    RT_STAT(23, 1);  // packet walks (camera and bounce-0 shadow rays)
     while (idx < end) {
+        RT_STAT(31, 1);
         const uint4 e = cn[idx];
         const bool inner = (e.w & 0x80000000u) != 0u;  // wave-uniform
         const bool h = lds_node_hit(e, rb, tmin, best);
@@ -487,7 +489,9 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
     uint32_t idx = wave_uniform(octant(d)) * nN;
     const uint32_t end = idx + nN;
     bool found = false;
+    RT_STAT(23, 1);  // packet walks (camera and bounce-0 shadow rays)
     while (idx < end) {
+        RT_STAT(31, 1);
         const uint4 e = cn[idx];
         const bool inner = (e.w & 0x80000000u) != 0u;
         const bool h = !found && lds_node_hit(e, rb, tmin, tmax);
@@ -513,6 +517,11 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
 // the parked leaves are tested once they are >= 1/kTriParkDen of the live lanes
 // (100k triangles: 1/4 738, 1/2 701, 3/4 570, 1/8 707 Msamples/s)
 constexpr int kTriParkDen = 4;
+// RT_TRI_LOOKAHEAD: the next sequential entry requested one step early
+// (100k triangles 888 -> 787 Msamples/s: 4 more VGPRs, 20 spilled; off)
+#ifndef RT_TRI_LOOKAHEAD
+#define RT_TRI_LOOKAHEAD 0
+#endif
 template <bool ANY>
 __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, const float4* __restrict__ tri,
                                               const uint32_t* __restrict__ perm, uint32_t nN, f3 o, f3 d,
@@ -523,11 +532,38 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
     const uint32_t end = idx + nN;
     if (ANY && id >= 0) idx = end;
     uint32_t leaf = kNone;
+    [[maybe_unused]] constexpr int ST = ANY ? 24 : 16;  // the sphere_walk slots (no spheres here)
+    RT_STAT(ST, 1);
+    RT_STAT(ST + 1, __popcll(__ballot(1)));
+#if RT_TRI_LOOKAHEAD
+    // one entry of lookahead: `seq` is the entry after the current one, loaded
+    // one step early, so a step that goes on to idx + 1 (a box hit, or a
+    // missed leaf) finds its entry already requested
+    const uint32_t last = end - 1u;
+    uint4 cur = cn[idx < last ? idx : last];
+    uint4 seq = cn[idx + 1u < last ? idx + 1u : last];
+#endif
     for (;;) {
         for (;;) {
             const bool adv = idx < end && leaf == kNone;
             if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
+            RT_STAT(ST + 2, 1);
+            RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(adv)));
             if (adv) {
+#if RT_TRI_LOOKAHEAD
+                const uint4 e = cur;
+                const bool inner = (e.w & 0x80000000u) != 0u;
+                const bool h = lds_node_hit_nf(e, rb, tmin, best);
+                if (h && !inner) leaf = e.w;
+                if (h || !inner) {
+                    idx = idx + 1u;
+                    cur = seq;
+                } else {
+                    idx = e.w & 0x7FFFFFFFu;
+                    cur = cn[idx < last ? idx : last];
+                }
+                seq = cn[idx + 1u < last ? idx + 1u : last];
+#else
                 const uint4 e = cn[idx];
                 const bool inner = (e.w & 0x80000000u) != 0u;
                 if (!lds_node_hit_nf(e, rb, tmin, best)) {
@@ -536,12 +572,15 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
                     if (!inner) leaf = e.w;
                     idx = idx + 1;
                 }
+#endif
             }
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
             if (kTriParkDen * parked >= live) break;
         }
         if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
+        RT_STAT(ST + 5, 1);
+        RT_STAT(ST + 6, __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone)));
         if (leaf != kNone) {
             if (ANY) {
                 if (tri_leaf_any(tri, leaf, o, d, tmin, best)) {

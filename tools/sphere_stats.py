@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Sphere-walk counters of a -DRT_STATS build (RTPT_LIB=variants/librtpt_stats.so)
-on the config-4 scene:  tools/sphere_stats.py [W H SPP [N_SPHERES]]"""
+"""Per-lane BVH walk counters of a -DRT_STATS build (RTPT_LIB=abvar/librtpt_stats.so)
+on the config-4 scene, or on the random-triangle scene with a 5th argument:
+  tools/sphere_stats.py [W H SPP [N [triangles]]]
+(sphere_walk and tri_cbvh_walk share the slots; a triangle scene has no spheres)"""
 import ctypes
 import json
 import os
@@ -12,8 +14,10 @@ from gpuraytracer_amd import RenderParams, Options, Renderer, Scene, lib  # noqa
 
 a = sys.argv[1:]
 W, H, SPP = (int(a[0]), int(a[1]), int(a[2])) if len(a) >= 3 else (480, 270, 16)
-NS = int(a[3]) if len(a) >= 4 else 1000
-with Renderer(Scene.random_spheres(W, H, NS, seed=42), options=Options.from_env()) as r:
+TRI = len(a) >= 5 and a[4] == "triangles"
+NS = int(a[3]) if len(a) >= 4 else (100000 if TRI else 1000)
+scene = Scene.random_triangles(W, H, NS, seed=7) if TRI else Scene.random_spheres(W, H, NS, seed=42)
+with Renderer(scene, options=Options.from_env()) as r:
     r.render(RenderParams(spp=SPP, bounces=3))
     st = (ctypes.c_uint64 * 32)()
     assert lib.rt_debug_stats(r._ctx, st, 32) == 0, lib.rt_last_error(r._ctx)
