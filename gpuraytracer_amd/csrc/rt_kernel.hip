@@ -686,7 +686,7 @@ void path_trace_kernel(KParams P) {
             }
         }
 #ifdef RT_STATS
-        if (!SPH) {
+        if (!SPH && GEO != kGeoTriBvh) {  // 24-31: the BVH any-hit walks' there
             RT_STAT(24, clock64() - t_round);
             RT_STAT(25, 1);
         }

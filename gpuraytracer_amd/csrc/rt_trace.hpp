@@ -528,7 +528,11 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
                                               float tmin, float& best, int& id) {
     constexpr uint32_t kNone = 0xFFFFFFFFu;
     const RayBox rb = ray_box(o, d);
+#if RT_TRI_ONE_LAYOUT  // experiment: every lane in the octant-0 layout (min/max box test)
+    uint32_t idx = 0;
+#else
     uint32_t idx = octant(d) * nN;
+#endif
     const uint32_t end = idx + nN;
     if (ANY && id >= 0) idx = end;
     uint32_t leaf = kNone;
@@ -566,7 +570,11 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
 #else
                 const uint4 e = cn[idx];
                 const bool inner = (e.w & 0x80000000u) != 0u;
+#if RT_TRI_ONE_LAYOUT
+                if (!lds_node_hit(e, rb, tmin, best)) {
+#else
                 if (!lds_node_hit_nf(e, rb, tmin, best)) {
+#endif
                     idx = inner ? (e.w & 0x7FFFFFFFu) : idx + 1;
                 } else {
                     if (!inner) leaf = e.w;

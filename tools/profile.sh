@@ -45,5 +45,9 @@ run sq_insts --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAV
 run sq_cycles --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-include-regex $KRE
 run sq_valu --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_CVT --kernel-include-regex $KRE
 run sq_lds --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_WAIT_INST_LDS --kernel-include-regex $KRE
+# vector-memory pipeline: address / tag processing of the per-lane node loads
+run ta --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum --kernel-include-regex $KRE
+run tcp --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum --kernel-include-regex $KRE
+run td --pmc TD_TD_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum --kernel-include-regex $KRE
 python3 "$R/tools/summarize_profile.py" "$OUT" "${BENCH[@]:1}" > "$OUT/summary.json"
 cat "$OUT/summary.json"
