@@ -55,6 +55,8 @@ struct rt_ctx {
     uint32_t mis_tab_S = 0;        // samples per strategy it was built for
     void* d_out8 = nullptr;        // staging for host RGBA8 outputs
     size_t out8_cap = 0;
+    void* d_mis_part = nullptr;    // per-ray MIS results of a split launch (rt_mis.hip)
+    size_t mis_part_cap = 0;
     uint32_t* d_seeds = nullptr;
     bool seeds_ready = false;
     uint32_t seed_max = 0xFFFFFFFFu;  // max seed value (bounds the Halton index)
@@ -143,6 +145,7 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_mis_shade);
     (void)hipFree(c->d_mis_tab);
     (void)hipFree(c->d_out8);
+    (void)hipFree(c->d_mis_part);
     (void)hipFree(c->d_seeds);
     (void)hipFree(c->d_sum);
     (void)hipFree(c->d_out);
@@ -546,6 +549,11 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
     K.row_start = start;
     K.row_step = step;
     K.row_count = count;
+    if (const size_t pb = rt::mis_part_bytes(K.camera_rays, pixels)) {
+        if ((st = ensure_staging(c, &c->d_mis_part, &c->mis_part_cap, pb, "hipMalloc(mis rays)")) != RT_OK)
+            return st;
+        K.part = reinterpret_cast<float4*>(c->d_mis_part);
+    }
 
     hipError_t e;
     (void)hipEventRecord(c->ev0, c->stream);

@@ -364,10 +364,12 @@ __device__ __forceinline__ f3 mis_shade_hit(const MisParams& P, const SceneView&
 
 }  // namespace
 
-// lanes per pixel: 3 (19.3 ms per reference frame: two rounds of the 6 camera
-// rays; 2 lanes 20.3, 6 lanes 19.8, 1 lane 26.1, 4 lanes 25.7)
+// lanes per pixel: 2 with split launches (17.64 ms per reference frame: three
+// rounds of the 6 camera rays, one workgroup per round; 3 lanes 17.89, 1 lane
+// 18.02; without the split 3 lanes 18.82 -- round 3: 2 lanes 20.3, 6 lanes
+// 19.8, 1 lane 26.1, 4 lanes 25.7)
 #ifndef RT_MIS_LANES
-#define RT_MIS_LANES 3
+#define RT_MIS_LANES 2
 #endif
 constexpr uint32_t kMisLanes = RT_MIS_LANES;
 // A wave holds 64 / ML pixels: an 8 x (8 / ML) tile when ML divides 8, else one
@@ -386,7 +388,32 @@ constexpr int kMisWavesPerEu = RT_MIS_WAVES;
 // reference scene has none; with FREEP false their loop is compiled out, which
 // also drops the one VGPR its loop-invariant test occupied (8 B of scratch at
 // 7 waves/SIMD, round 4).
-template <int GEO, bool FREEP = true>
+// The pixel's stored value (:688-706 and textBuffer :705): the sum over its
+// camera rays and their count; RGBA8 after exposure, Reinhard, clamp, gamma.
+__device__ __forceinline__ void mis_store(const MisParams& P, size_t o, f3 acc) {
+    const float nc = (float)P.camera_rays;
+    if (P.out) P.out[o] = make_float4(acc.x, acc.y, acc.z, nc);  // textBuffer (:705) + count
+    if (P.out8) {
+        // :688-706: exposure, Reinhard, clamp, gamma 1/2.2, uchar(c * 255)
+        const float e[3] = {(acc.x / nc) * P.exposure, (acc.y / nc) * P.exposure,
+                            (acc.z / nc) * P.exposure};
+        unsigned char c8[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float tm = clamp01(e[k] / (e[k] + 1.0f));
+            const float g = pow_pt(tm, 1.0f / 2.2f);
+            c8[k] = (unsigned char)(g * 255.0f);
+        }
+        P.out8[o] = make_uchar4(c8[0], c8[1], c8[2], 255);
+    }
+}
+
+// SPLIT: one workgroup per (tile, round) -- blockIdx.z is the round -- and every
+// lane stores its camera ray's result (c, has) to P.part[i][pixel]; mis_sum_kernel
+// then adds a pixel's rays in order i.  Twice the workgroups of half the length:
+// the frame's last workgroups (the tail, when too few are left to fill the GPU)
+// end sooner.
+template <int GEO, bool FREEP = true, bool SPLIT = false>
 __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisParams P) {
     extern __shared__ float4 lds[];
     SceneView sv;
@@ -474,7 +501,8 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
         st[8 * kBlockThreads + k] = 0.0f;
     }
     const uint32_t rounds = (P.camera_rays + ML - 1u) / ML;
-    for (uint32_t r = 0; r < rounds; ++r) {  // :652
+    const uint32_t r_begin = SPLIT ? blockIdx.z : 0u, r_end = SPLIT ? blockIdx.z + 1u : rounds;
+    for (uint32_t r = r_begin; r < r_end; ++r) {  // :652
         const uint32_t tid = opaque_u32(threadIdx.x);
         const uint32_t sub = (tid & 63u) % ML;  // ML need not divide 64
         const uint32_t i = r * ML + sub;
@@ -517,6 +545,16 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
                 }
             }
         }
+        if (SPLIT) {  // this ray's result; the pixel's sum is mis_sum_kernel's
+            if (i < P.camera_rays) {
+                uint32_t x, j;
+                pixel_of(opaque_u32(threadIdx.x), x, j);
+                const size_t npix = (size_t)P.row_count * (size_t)P.W;
+                P.part[(size_t)i * npix + (size_t)j * (size_t)P.W + x] =
+                    make_float4(c.x, c.y, c.z, has ? 1.0f : 0.0f);
+            }
+            continue;
+        }
         const uint32_t t2 = opaque_u32(threadIdx.x);
         float* st = sv.xstash;
         f3 acc{st[6 * kBlockThreads + t2], st[7 * kBlockThreads + t2], st[8 * kBlockThreads + t2]};
@@ -536,31 +574,42 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
         st[7 * kBlockThreads + t2] = acc.y;
         st[8 * kBlockThreads + t2] = acc.z;
     }
+    if (SPLIT) return;
     const uint32_t tl = opaque_u32(threadIdx.x);
     const f3 acc{sv.xstash[6 * kBlockThreads + tl], sv.xstash[7 * kBlockThreads + tl],
                  sv.xstash[8 * kBlockThreads + tl]};
-    const float nc = (float)P.camera_rays;
     if ((opaque_u32(threadIdx.x) & 63u) % ML != 0) return;  // the group leader stores the pixel
     uint32_t x, j;
     pixel_of(opaque_u32(threadIdx.x), x, j);
-    const size_t o = (size_t)j * (size_t)P.W + x;
-    if (P.out) P.out[o] = make_float4(acc.x, acc.y, acc.z, nc);  // textBuffer (:705) + count
-    if (P.out8) {
-        // :688-706: exposure, Reinhard, clamp, gamma 1/2.2, uchar(c * 255)
-        const float e[3] = {(acc.x / nc) * P.exposure, (acc.y / nc) * P.exposure,
-                            (acc.z / nc) * P.exposure};
-        unsigned char c8[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float tm = clamp01(e[k] / (e[k] + 1.0f));
-            const float g = pow_pt(tm, 1.0f / 2.2f);
-            c8[k] = (unsigned char)(g * 255.0f);
-        }
-        P.out8[o] = make_uchar4(c8[0], c8[1], c8[2], 255);
+    mis_store(P, (size_t)j * (size_t)P.W + x, acc);
+}
+
+// The pixel sums of a SPLIT launch: the camera rays' results added in ray order
+// (:652-677, the same additions as the in-kernel sum), then the store.
+__global__ void mis_sum_kernel(MisParams P) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+    if (x >= (uint32_t)P.W) return;
+    const size_t npix = (size_t)P.row_count * (size_t)P.W, o = (size_t)j * (size_t)P.W + x;
+    f3 acc{0.0f, 0.0f, 0.0f};
+    for (uint32_t i = 0; i < P.camera_rays; ++i) {
+        const float4 v = P.part[(size_t)i * npix + o];
+        if (v.w != 0.0f) acc = acc + f3{v.x, v.y, v.z};
     }
+    mis_store(P, o, acc);
 }
 
 constexpr size_t kMisStashBytes = 15u * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc, strategy sum
+
+// SPLIT launches (RT_MIS_SPLIT): the per-ray results buffer, 16 B per camera ray
+// and pixel; 0 (no split) when it would exceed kMisPartMax or the split is off.
+#ifndef RT_MIS_SPLIT
+#define RT_MIS_SPLIT 1
+#endif
+constexpr size_t kMisPartMax = (size_t)1 << 30;
+size_t mis_part_bytes(uint32_t camera_rays, size_t pixels) {
+    const size_t b = (size_t)camera_rays * pixels * sizeof(float4);
+    return (RT_MIS_SPLIT && camera_rays > kMisLanes && b <= kMisPartMax) ? b : 0u;
+}
 
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + shading records
     return (size_t)((n_pairs ? kPairF4 * n_pairs : 3u * n_tri) + 3u * n_tri) * sizeof(float4);
@@ -570,17 +619,28 @@ size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs) {  // scene records + sha
 // fit the 64 KB of the LDS layouts keeps them with the 15 KB stash on top
 // (up to 79 KB per workgroup, fewer workgroups per CU) instead of dropping to
 // the global-memory kernel.
-template <int GEO, bool FREEP = true>
-hipError_t launch_mis_g(const MisParams& P, size_t lds, hipStream_t stream) {
+template <int GEO, bool FREEP, bool SPLIT>
+hipError_t launch_mis_s(const MisParams& P, size_t lds, hipStream_t stream) {
     constexpr uint32_t TX = kMisTile ? 16u : kMisRowPixels, TY = kMisTile ? 2u * (8u / kMisLanes) : 4u;
-    const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY);  // workgroup: TX x TY pixels
+    const uint32_t rounds = (P.camera_rays + kMisLanes - 1u) / kMisLanes;
+    // workgroup: TX x TY pixels (x one round when SPLIT)
+    const dim3 grid((P.W + TX - 1) / TX, (P.row_count + TY - 1) / TY, SPLIT ? rounds : 1u);
     if (lds > 65536) {
-        const hipError_t e = hipFuncSetAttribute((const void*)mis_kernel<GEO, FREEP>,
+        const hipError_t e = hipFuncSetAttribute((const void*)mis_kernel<GEO, FREEP, SPLIT>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((mis_kernel<GEO, FREEP>), grid, dim3(kBlockThreads), lds, stream, P);
+    hipLaunchKernelGGL((mis_kernel<GEO, FREEP, SPLIT>), grid, dim3(kBlockThreads), lds, stream, P);
+    if (SPLIT) {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(mis_sum_kernel, dim3((P.W + 255) / 256, P.row_count), dim3(256), 0, stream, P);
+    }
     return hipGetLastError();
+}
+template <int GEO, bool FREEP = true>
+hipError_t launch_mis_g(const MisParams& P, size_t lds, hipStream_t stream) {
+    return P.part ? launch_mis_s<GEO, FREEP, true>(P, lds, stream) : launch_mis_s<GEO, FREEP, false>(P, lds, stream);
 }
 
 hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream) {

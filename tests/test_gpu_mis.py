@@ -44,7 +44,7 @@ def test_mis_golden_fixture_bit_exact():
     assert_same(out8, g["out8"], "rgba8")
 
 
-@pytest.mark.parametrize("rays,samples", [(1, 3), (2, 30), (3, 31)])
+@pytest.mark.parametrize("rays,samples", [(1, 3), (2, 30), (3, 31), (5, 12), (7, 9)])
 def test_mis_vs_oracle(rays, samples):
     s = Scene.cornell_box_mis(72, 40)  # not a multiple of the 16x16 tile
     with Renderer(s) as r:
