@@ -327,7 +327,11 @@ typedef struct rt_mis_params {
  *   plus the divisor.
  * out_rgba8 (optional): the reference's pixels (:248-257,688-706): exposure
  *   1/(1.2*2^ev100), Reinhard, clamp, gamma 1/2.2, uchar(c*255), alpha 255.
- * At least one output must be non-null.  Synchronous. */
+ * At least one output must be non-null.  Synchronous.  When camera_rays is
+ * above the kernel's lanes per pixel (2) the frame runs as one workgroup per
+ * round of camera rays and an ordered per-pixel sum: the context then keeps a
+ * device buffer of 16 B per camera ray and pixel (46 MB at 800x600 x 6; frames
+ * that would need more than 1 GB run without the split). */
 int rt_render_mis(rt_ctx* ctx, const rt_mis_params* params, float* out_rgba32f,
                   uint8_t* out_rgba8);
 
