@@ -78,6 +78,26 @@ def test_mis_row_tiles_equal_full_frame_and_rtrace_scene():
     assert_same(full, ref, "sum")
 
 
+def test_mis_frame_without_split_equals_split_rows():
+    """A frame whose per-ray buffer would pass 1 GB (rt_mis.hip kMisPartMax) runs
+    without the split: the kernel adds the rounds of camera rays itself (2 rounds
+    of 2 lanes here).  Rows of that frame equal the same rows rendered through the
+    split launch (per-ray buffer + ordered sum kernel) and the oracle."""
+    W = H = 4800
+    rays = 3
+    assert W * H * rays * 16 > (1 << 30)
+    s = Scene.cornell_box_mis(W, H)
+    p_rows = MisParams(camera_rays=rays, mis_samples=3, row_start=7, row_step=997)
+    with Renderer(s) as r:
+        full, full8 = r.render_mis(MisParams(camera_rays=rays, mis_samples=3))
+        rows, rows8 = r.render_mis(p_rows)
+    assert_same(full[7::997], rows, "frame rows vs split rows")
+    assert_same(full8[7::997], rows8, "frame rows vs split rows (rgba8)")
+    ref, ref8 = oracle_lib.render_mis(s, rays, 3, row_start=7, row_step=997)
+    assert_same(rows, ref, "split rows vs oracle")
+    assert_same(rows8, ref8, "split rows vs oracle (rgba8)")
+
+
 def test_mis_device_outputs_match_host():
     import torch
     s = Scene.cornell_box_mis(40, 24)
