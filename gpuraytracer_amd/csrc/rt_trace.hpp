@@ -515,8 +515,12 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
 // test AND the three record loads and the test of a triangle.  Per lane the
 // entries are visited in the same order and ranked by (t, id): the same result.
 // the parked leaves are tested once they are >= 1/kTriParkDen of the live lanes
-// (100k triangles: 1/4 738, 1/2 701, 3/4 570, 1/8 707 Msamples/s)
-constexpr int kTriParkDen = 4;
+// (100k triangles: 1/4 738, 1/2 701, 3/4 570, 1/8 707 Msamples/s; round 5 with
+// near/far boxes: 1/3 894-896, 1/4 887-890, 1/2 872, 1/6 865, 1/8 843)
+#ifndef RT_TRI_PARK_DEN
+#define RT_TRI_PARK_DEN 3
+#endif
+constexpr int kTriParkDen = RT_TRI_PARK_DEN;
 // RT_TRI_LOOKAHEAD: the next sequential entry requested one step early
 // (100k triangles 888 -> 787 Msamples/s: 4 more VGPRs, 20 spilled; off)
 #ifndef RT_TRI_LOOKAHEAD
