@@ -347,8 +347,12 @@ __device__ __forceinline__ bool lds_node_hit_nf(const uint4& e, const RayBox& rb
 // value is sph_test's, ranked by (t, id): the same result.  ANY: *id becomes
 // >= 0 on the first accepted hit (and that lane stops).
 // the parked roots run once they are >= 1/kSphParkDen of the live lanes
-// (config 4: 2 157.3 ms, 4 158.4, 6 161.1)
-constexpr int kSphParkDen = 2;
+// (config 4: 2 157.3 ms, 4 158.4, 6 161.1; round 5: 3 149.7-149.8, 2 150.2-150.3,
+// 1 207.4)
+#ifndef RT_SPH_PARK_DEN
+#define RT_SPH_PARK_DEN 3
+#endif
+constexpr int kSphParkDen = RT_SPH_PARK_DEN;
 template <bool ANY>
 __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const uint16_t* __restrict__ ids,
                                             uint32_t nN, uint32_t nT, f3 o, f3 d, float tmin, float& best,
