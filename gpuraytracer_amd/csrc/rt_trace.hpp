@@ -348,9 +348,9 @@ __device__ __forceinline__ bool lds_node_hit_nf(const uint4& e, const RayBox& rb
 // >= 0 on the first accepted hit (and that lane stops).
 // the parked roots run once they are >= 1/kSphParkDen of the live lanes
 // (config 4: 2 157.3 ms, 4 158.4, 6 161.1; round 5: 3 149.7-149.8, 2 150.2-150.3,
-// 1 207.4)
+// 1 207.4 -- 1/2 kept: with 1/3 the profiled HBM traffic rose from 69 to 110 MB)
 #ifndef RT_SPH_PARK_DEN
-#define RT_SPH_PARK_DEN 3
+#define RT_SPH_PARK_DEN 2
 #endif
 constexpr int kSphParkDen = RT_SPH_PARK_DEN;
 template <bool ANY>
