@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTPT_LIB overrides the in-tree library (A/B builds of the kernel).
 library_path = os.environ.get("RTPT_LIB") or os.path.join(_HERE, "librtpt.so")
@@ -96,7 +96,7 @@ class CreateOptions(ctypes.Structure):  # rt_create_options
                 ("tri_bvh_build", ctypes.c_uint32), ("tri_leaf_max", ctypes.c_uint32),
                 ("tri_leaf_cost", ctypes.c_float), ("sphere_leaf_max", ctypes.c_uint32),
                 ("sphere_median", ctypes.c_uint32), ("walk_scheduler", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32 * 8)]
+                ("walk_leaf_den", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 7)]
 
 
 assert ctypes.sizeof(CreateOptions) == 64
@@ -126,7 +126,8 @@ class LaunchInfo(ctypes.Structure):  # rt_launch_info
 
 class BuildStats(ctypes.Structure):  # rt_build_stats
     _fields_ = [("tri_bvh_build", ctypes.c_uint32), ("tri_bvh_nodes", ctypes.c_uint32),
-                ("tri_bvh_build_ms", ctypes.c_float), ("scene_compile_ms", ctypes.c_float)]
+                ("tri_bvh_build_ms", ctypes.c_float), ("scene_compile_ms", ctypes.c_float),
+                ("tri_bvh_temp_kib", ctypes.c_uint32)]
 
 
 class TileLayout(ctypes.Structure):  # rt_tile_layout_info

@@ -23,9 +23,9 @@
 #include "rt_kernel.hpp"
 #include "rt_scene.hpp"
 
-// RT_TRI_BVH_DEFAULT resolves to this build: the GPU binned SAH renders at the
-// host build's rate (100k triangles 846.6 vs 844.4, 1M 167.6 vs 167.6
-// Msamples/s) and builds in 33 vs 125 ms (100k), 329 vs 1383 ms (1M)
+// RT_TRI_BVH_DEFAULT resolves to this build: the GPU binned SAH builds the host
+// build's tree (same rules, same render rate) in a tenth of the time or less --
+// the measured build times and rates are in DESIGN.md §5 and profiles/
 constexpr uint32_t kDefaultTriBuild = RT_TRI_BVH_GPU_SAH;
 
 struct rt_ctx {
@@ -49,6 +49,7 @@ struct rt_ctx {
     uint32_t tri_bvh_nodes = 0;      // per layout
     uint32_t tri_bvh_build_used = 0; // rt_tri_bvh_build of the built tree (0: none)
     float tri_bvh_build_ms = 0.0f;   // wall time of the triangle-BVH build
+    size_t tri_bvh_temp_bytes = 0;   // peak temporaries of the GPU SAH build
     float scene_compile_ms = 0.0f;   // host scene compile (rt_scene.cpp compile_scene)
     float4* d_mis_shade = nullptr;
     float4* d_mis_tab = nullptr;   // Halton table of the MIS integrator
@@ -82,6 +83,7 @@ struct rt_ctx {
     uint32_t lanes = 0;  // rt_create_options.lanes_per_pixel (0 = auto)
     rt::SceneMem scene_mem = rt::SceneMem::kAuto;  // rt_create_options.scene_layout
     uint32_t walk = 0;   // rt_create_options.walk_scheduler
+    uint32_t walk_leaf_den = 0;  // rt_create_options.walk_leaf_den
     std::string err;
 };
 
@@ -276,6 +278,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.flags = ((p->flags & RT_OUT_FP16) ? rt::kOutFp16 : 0u) | ((p->flags & RT_OUT_RGBA8) ? rt::kOutRgba8 : 0u);
     K.lanes = c->lanes;
     K.walk = c->walk;
+    K.walk_leaf_den = c->walk_leaf_den;
     {
         const uint64_t imax = (uint64_t)c->seed_max + p->sample_base + (p->spp ? p->spp - 1u : 0u);
         K.max_index = imax > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)imax;
@@ -575,7 +578,7 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
 // rt_create_options (include/rtpt.h) -> the context's choices and the host
 // builds' options.  False (with *why) for a value outside its range.
 struct Resolved {
-    uint32_t lanes = 0, tri_build = RT_TRI_BVH_HOST_SAH, walk = RT_WALK_AUTO;
+    uint32_t lanes = 0, tri_build = RT_TRI_BVH_HOST_SAH, walk = RT_WALK_AUTO, walk_leaf_den = 0;
     rt::SceneMem mem = rt::SceneMem::kAuto;
     uint32_t tri_leaf_max = rt::kTriLeafMax;
     double tri_leaf_cost = 1.0;
@@ -622,6 +625,8 @@ bool resolve_options(const rt_create_options* o, Resolved* r, const char** why) 
     r->build.sphere_sah = o->sphere_median == 0;
     if (o->walk_scheduler > RT_WALK_SORTED) { *why = "rt_create_options.walk_scheduler out of range"; return false; }
     r->walk = o->walk_scheduler;
+    if (o->walk_leaf_den > 64) { *why = "rt_create_options.walk_leaf_den must be <= 64"; return false; }
+    r->walk_leaf_den = o->walk_leaf_den;
     return true;
 }
 
@@ -679,6 +684,7 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
     c->tri_build = ro.tri_build;
     c->scene_mem = ro.mem;
     c->walk = ro.walk;
+    c->walk_leaf_den = ro.walk_leaf_den;
     DeviceGuard g(c->device);
     const char* err = nullptr;
     using clk = std::chrono::steady_clock;
@@ -733,13 +739,16 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
                     status = RT_ERR_OUT_OF_MEMORY; msg = std::string("hipMalloc(triangle BVH): ") + hipGetErrorString(e); break;
                 }
                 uint32_t total = 0;
+                size_t temp = 0;
                 if ((e = rt::build_tri_gsah(c->d_tri_isect, nT, s.margin, ro.tri_leaf_max, ro.tri_leaf_cost,
-                                            c->d_tri_nodes, c->d_tri_sorted, c->d_tri_perm, &total,
+                                            c->d_tri_nodes, c->d_tri_sorted, c->d_tri_perm, &total, &temp,
                                             c->stream)) != hipSuccess) {
-                    status = (e == hipErrorInvalidValue) ? RT_ERR_INVALID_ARG : RT_ERR_LAUNCH;
+                    status = (e == hipErrorInvalidValue) ? RT_ERR_INVALID_ARG
+                             : (e == hipErrorOutOfMemory) ? RT_ERR_OUT_OF_MEMORY : RT_ERR_LAUNCH;
                     msg = std::string("triangle BVH build: ") + hipGetErrorString(e); break;
                 }
                 c->tri_bvh_nodes = total;
+                c->tri_bvh_temp_bytes = temp;
             } else if (c->tri_build == RT_TRI_BVH_GPU_LBVH) {  // GPU Morton build (rt_lbvh.hip)
                 if ((e = hipMalloc((void**)&c->d_tri_nodes, rt::kTriCompactLayouts * nn * sizeof(uint4))) != hipSuccess ||
                     (e = hipMalloc((void**)&c->d_tri_sorted, 3 * (size_t)nT * sizeof(float4))) != hipSuccess ||
@@ -933,6 +942,7 @@ int rt_build_info(const rt_ctx* c, rt_build_stats* info) {
     info->tri_bvh_nodes = c->tri_bvh_nodes;
     info->tri_bvh_build_ms = c->tri_bvh_build_ms;
     info->scene_compile_ms = c->scene_compile_ms;
+    info->tri_bvh_temp_kib = (uint32_t)((c->tri_bvh_temp_bytes + 1023) / 1024);
     return RT_OK;
 }
 

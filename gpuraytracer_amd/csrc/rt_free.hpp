@@ -125,6 +125,33 @@ __device__ __forceinline__ float halton_bounce(uint32_t i, int b) {
     }
 }
 
+// Event log of a -DRT_FREE_DEBUG diagnostic build (read with rt_debug_stats):
+// slots 0/1 record every query start, leaf resolve, query end and sample end
+// of the pixels (RT_FREE_DBG_X0, _Y0) and (_X1, _Y1); slot 2 records parked
+// leaves whose walk-loop resolve disagrees with the same arithmetic evaluated
+// before the branch (RT_FREE_CHECK).  Record = kFreeDbgRec words.
+#ifdef RT_FREE_DEBUG
+#ifndef RT_FREE_DBG_X0
+#define RT_FREE_DBG_X0 18
+#define RT_FREE_DBG_Y0 20
+#define RT_FREE_DBG_X1 29
+#define RT_FREE_DBG_Y1 24
+#endif
+constexpr int kFreeDbgRec = 12, kFreeDbgMax = 1024;
+__device__ uint32_t g_free_dbg[4 + 3 * kFreeDbgMax * kFreeDbgRec];
+__device__ __forceinline__ void free_dbg(int slot, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                         float f4, float f5, float f6, float f7, float f8, float f9,
+                                         float f10, float f11) {
+    const uint32_t pos = atomicAdd(&g_free_dbg[slot], 1u);
+    if (pos >= (uint32_t)kFreeDbgMax) return;
+    uint32_t* r = &g_free_dbg[4 + ((uint32_t)slot * kFreeDbgMax + pos) * kFreeDbgRec];
+    r[0] = w0; r[1] = w1; r[2] = w2; r[3] = w3;
+    r[4] = __float_as_uint(f4); r[5] = __float_as_uint(f5); r[6] = __float_as_uint(f6);
+    r[7] = __float_as_uint(f7); r[8] = __float_as_uint(f8); r[9] = __float_as_uint(f9);
+    r[10] = __float_as_uint(f10); r[11] = __float_as_uint(f11);
+}
+#endif
+
 // One-wave workgroups (as the lockstep sphere kernel: a workgroup's wave slots
 // are released when its wave ends).
 constexpr uint32_t kFreeThreads = 64;
@@ -136,11 +163,8 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
     constexpr bool SPH = GEO == kGeoSphLds;
     // parked leaves are tested once they are >= 1/kLeafDen of the walking lanes
     // (the lockstep walks' kSphParkDen / kTriParkDen)
-#ifdef RT_FREE_LEAF_DEN
-    constexpr int kLeafDen = RT_FREE_LEAF_DEN;
-#else
-    constexpr int kLeafDen = SPH ? kSphParkDen : kTriParkDen;
-#endif
+    // (rt_create_options.walk_leaf_den; 1: only when every walker is parked)
+    const int kLeafDen = P.walk_leaf_den ? (int)P.walk_leaf_den : (SPH ? kSphParkDen : kTriParkDen);
     extern __shared__ float4 lds[];
     __shared__ uint32_t seed_s[kFreeThreads];
     __shared__ float stash[kFsSlots * kFreeThreads];
@@ -235,15 +259,36 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
     RayBox rb{};
     const f3 cu = ld_f3(P.cam_u), cv = ld_f3(P.cam_v), cw = ld_f3(P.cam_w);
     const float fW = (float)P.W, fH = (float)P.H;
+#ifdef RT_FREE_DEBUG
+    int dslot = -1;  // this lane's log slot (0/1 for the two watched pixels)
+    {
+        uint32_t x, j;
+        pixel_of(threadIdx.x, x, j);
+        const uint32_t y = P.row_start + j * P.row_step;
+        if (x == RT_FREE_DBG_X0 && y == RT_FREE_DBG_Y0) dslot = 0;
+        if (x == RT_FREE_DBG_X1 && y == RT_FREE_DBG_Y1) dslot = 1;
+    }
+#define FREE_LOG(...) \
+    do {                                 \
+        if (dslot >= 0) free_dbg(dslot, __VA_ARGS__); \
+    } while (0)
+#else
+#define FREE_LOG(...) ((void)0)
+#endif
 
     // the expensive part of a parked leaf's test: the IEEE roots of sph_test
     // (shaders_old.metal:108-136) or the leaf's exact triangle tests
-    auto resolve_leaf = [&]() {
+    auto resolve_leaf = [&](uint32_t site) {
+        (void)site;
         if constexpr (SPH) {
             const float sq = sqrtf(pdisc);
             const float a2 = 2.0f * a;
             float t = (-pb - sq) / a2;
             if (!(t > tmin)) t = (-pb + sq) / a2;
+#ifdef RT_FREE_DEBUG
+            const float best0 = best;
+            const int id0 = id;
+#endif
             if (ph == kFpShadow) {
                 if (t > tmin && t < best) {
                     id = 0;
@@ -256,6 +301,9 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
                     id = s;
                 }
             }
+            FREE_LOG(2u | (uint32_t)ph << 8 | (uint32_t)b << 16 | site << 24, n, leaf,
+                     sv.nT + sv.sid[leaf], pb, pdisc, a, t, best0, __int_as_float(id0), best,
+                     __int_as_float(id));
         } else {
             if (ph == kFpShadow) {
                 if (tri_leaf_any(sv.tsorted, leaf, o, d, tmin, best)) {
@@ -292,8 +340,10 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
 #endif
         // a leaf parked at the end of its walk (the walk phase may stop before
         // the parked leaves reach their round)
-        if (leaf != kNone) resolve_leaf();
+        if (leaf != kNone) resolve_leaf(1u);
         const bool fin = ph <= kFpShadow && idx >= end;
+        if (fin) FREE_LOG(3u | (uint32_t)ph << 8 | (uint32_t)b << 16, n, idx, end, best, 0.0f, 0.0f, 0.0f,
+                          0.0f, 0.0f, 0.0f, __int_as_float(id));
         // (1) a finished shadow query: raytrace.metal:79-89, then the next bounce (:99-100)
         if (fin && ph == kFpShadow) {
             if (id < 0) st_set3(kFsAcc, st_get3(kFsAcc) + st_get3(kFsContrib));
@@ -378,6 +428,12 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
         // (3) the end of a sample: raytrace.metal:103, then the next sample's camera ray
         if (ph == kFpEnd) {
             if (n != 0xFFFFFFFFu) st_set3(kFsLum, st_get3(kFsLum) + st_get3(kFsAcc));  // :103 in order n
+#ifdef RT_FREE_DEBUG
+            if (n != 0xFFFFFFFFu) {
+                const f3 acc = st_get3(kFsAcc);
+                FREE_LOG(4u, n, 0u, 0u, acc.x, acc.y, acc.z, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f);
+            }
+#endif
             n += 1;
             if (n >= P.spp) {
                 ph = kFpDone;
@@ -425,6 +481,8 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
             end = idx + nLay;
             if (id >= 0 && shadow) idx = end;                      // occluded by a wall
             ph = shadow ? kFpShadow : kFpClosest;
+            FREE_LOG(1u | (uint32_t)ph << 8 | (uint32_t)b << 16, n, idx, end, o.x, o.y, o.z, d.x, d.y, d.z,
+                     best, __int_as_float(id));
             RT_STAT(26, __popcll(__ballot(1)));
         }
         const bool live = ph != kFpDone;
@@ -481,6 +539,43 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
             if (np > 0 && kLeafDen * np >= nwalk) {
                 RT_STAT(22, 1);
                 RT_STAT(23, np);
+#ifdef RT_FREE_BRANCH
+                if (true) {
+#ifdef RT_FREE_CHECK
+                    // the select form's arithmetic before the branch, compared after it
+                    float xb = best;
+                    int xi = id;
+                    uint32_t xx = idx;
+                    float xt = 0.0f;
+                    const uint32_t leaf0 = leaf;
+                    const float best0 = best;
+                    const int id0 = id;
+                    if (parked) {
+                        const float sq = sqrtf(pdisc);
+                        const float a2 = 2.0f * a;
+                        float t = (-pb - sq) / a2;
+                        const float t2 = (-pb + sq) / a2;
+                        t = (t > tmin) ? t : t2;
+                        xt = t;
+                        const int sidv = (int)(sv.nT + sv.sid[leaf]);
+                        if (ph == kFpShadow) {
+                            if (t > tmin && t < best) { xi = 0; xx = end; }
+                        } else if (t > tmin && t < 3.0e38f && t <= best && (t < best || sidv < id)) {
+                            xb = t;
+                            xi = sidv;
+                        }
+                    }
+#endif
+                    if (parked) resolve_leaf(0u);
+#ifdef RT_FREE_CHECK
+                    if (parked) atomicAdd(&g_free_dbg[3], 1u);  // resolves checked
+                    if (parked && (__float_as_uint(xb) != __float_as_uint(best) || xi != id || xx != idx)) {
+                        free_dbg(2, (uint32_t)ph | (uint32_t)b << 8, leaf0, (uint32_t)id0, (uint32_t)xi,
+                                 pb, pdisc, a, tmin, best0, xt, best, __int_as_float(id));
+                    }
+#endif
+                } else
+#endif
                 if constexpr (SPH) {
                     // every lane evaluates the roots, parked lanes keep the
                     // result: the branch form (resolve_leaf under `if (parked)`)
@@ -496,12 +591,19 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
                     const bool sh = ph == kFpShadow;
                     const bool hit_any = sh && t > tmin && t < best;
                     const bool hit_c = !sh && t > tmin && t < 3.0e38f && t <= best && (t < best || sidv < id);
+#ifdef RT_FREE_DEBUG
+                    const float best0 = best;
+                    const int id0 = id;
+#endif
                     id = (parked && hit_any) ? 0 : ((parked && hit_c) ? sidv : id);
                     idx = (parked && hit_any) ? end : idx;
                     best = (parked && hit_c) ? t : best;
+                    if (parked)
+                        FREE_LOG(2u | (uint32_t)ph << 8 | (uint32_t)b << 16 | 2u << 24, n, leaf, (uint32_t)sidv, pb,
+                                 pdisc, a, t, best0, __int_as_float(id0), best, __int_as_float(id));
                     leaf = kNone;
                 } else {
-                    if (parked) resolve_leaf();
+                    if (parked) resolve_leaf(0u);
                 }
             }
             const int nfin = nlive - __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone || (live && idx < end)));

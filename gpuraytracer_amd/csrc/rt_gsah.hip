@@ -84,6 +84,9 @@ __global__ void tri_box_kernel(const float4* __restrict__ tri, uint32_t n, float
 
 // bins of one slot: count[3][kBins], lo[3][kBins][3], hi[3][kBins][3]
 constexpr uint32_t kSlotWords = 3 * kBins * 7;
+// Bin slots at a time (2,688 B each: 176 MB): a level with more nodes that
+// can split runs its binning and split passes in batches of this many.
+constexpr uint32_t kMaxBinSlots = 65536;
 
 // The same binning with the bins of a chunk of kBinChunk consecutive positions
 // privatised in LDS when the whole chunk belongs to one node (every chunk of
@@ -160,15 +163,26 @@ __device__ __forceinline__ double area(const float* lo, const float* hi) {
     return x * y + y * z + z * x;
 }
 
-// One thread per node being split: the binned SAH of build_tri_sah.
+// One thread per node of the level: the binned SAH of build_tri_sah for the
+// nodes holding a bin slot of this batch; nodes of one triangle (which
+// cannot split and hold no slot) become leaves in the first batch.
 // split_flag[s] = 1 when the node splits (else it becomes a leaf).
 __global__ void split_kernel(uint32_t m, const uint32_t* __restrict__ active, GNode* __restrict__ nodes,
                              const uint32_t* __restrict__ bins, uint32_t leaf_max, double trav_cost,
-                             float margin, uint32_t* __restrict__ split_flag) {
+                             float margin, uint32_t* __restrict__ split_flag, uint32_t first_batch) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= m) return;
     GNode& N = nodes[active[s]];
-    const uint32_t* B = bins + (size_t)s * kSlotWords;
+    if (N.count <= 1) {
+        if (first_batch) {
+            N.leaf = 1;
+            N.axis = -1;
+            split_flag[s] = 0;
+        }
+        return;
+    }
+    if (N.slot == kNoSlot) return;  // another batch's node
+    const uint32_t* B = bins + (size_t)N.slot * kSlotWords;
     double best = INFINITY;
     int best_axis = -1, best_bin = 0;
     for (int a = 0; a < 3; ++a) {
@@ -375,9 +389,21 @@ __global__ void mark_kernel(uint32_t m, const uint32_t* __restrict__ list, const
     if (s < m) splitting[list[s]] = flag ? (uint8_t)flag[s] : (uint8_t)0;
 }
 
-__global__ void assign_slots_kernel(uint32_t m, const uint32_t* __restrict__ list, GNode* __restrict__ nodes) {
+// need[s] = 1 for a node of the level that can split (two or more triangles)
+__global__ void need_bins_kernel(uint32_t m, const uint32_t* __restrict__ list, const GNode* __restrict__ nodes,
+                                 uint32_t* __restrict__ need) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < m) nodes[list[s]].slot = s;
+    if (s < m) need[s] = nodes[list[s]].count > 1 ? 1u : 0u;
+}
+
+// bin slots of one batch: the nodes of need rank [b0, b0 + nb)
+__global__ void assign_slots_kernel(uint32_t m, const uint32_t* __restrict__ list, const uint32_t* __restrict__ need,
+                                    const uint32_t* __restrict__ rank, uint32_t b0, uint32_t nb,
+                                    GNode* __restrict__ nodes) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= m) return;
+    const uint32_t r = rank[s];
+    nodes[list[s]].slot = (need[s] && r >= b0 && r - b0 < nb) ? r - b0 : kNoSlot;
 }
 
 // ---- exclusive scan of uint32 (deterministic, three passes) ----------------
@@ -519,19 +545,20 @@ hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* til
 
 hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_t leaf_max, double trav_cost,
                           uint4* d_nodes, float4* d_sorted, uint32_t* d_perm, uint32_t* total_nodes,
-                          hipStream_t s) {
+                          size_t* temp_bytes, hipStream_t s) {
     *total_nodes = 0;
+    if (temp_bytes) *temp_bytes = 0;
     if (n == 0) return hipSuccess;
     if (n >= (1u << 24)) return hipErrorInvalidValue;  // leaf index field is 24 bits
     const uint32_t cap = 2 * n - 1;                    // nodes at most
     float *bl = nullptr, *bh = nullptr, *cen = nullptr;
     uint32_t *ids = nullptr, *ids2 = nullptr, *seg = nullptr, *seg2 = nullptr, *lflag = nullptr, *lscan = nullptr,
              *tiles = nullptr, *bins = nullptr, *split_flag = nullptr, *split_rank = nullptr, *lists = nullptr,
-             *size = nullptr, *pos = nullptr;
+             *size = nullptr, *pos = nullptr, *need = nullptr, *need_rank = nullptr;
     uint8_t* splitting = nullptr;
     GNode* nodes = nullptr;
     hipError_t e = hipSuccess;
-    size_t bins_cap = 0;
+    size_t bins_cap = 0, bins_peak = 0;  // words, bytes
     std::vector<uint32_t> level_off, level_cnt;  // node lists of every level (in `lists`)
     do {
         const uint32_t nt = (n + kScanTile - 1) / kScanTile + 1;
@@ -539,8 +566,12 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
             (e = dalloc(&ids, n)) || (e = dalloc(&ids2, n)) || (e = dalloc(&seg, n)) || (e = dalloc(&seg2, n)) ||
             (e = dalloc(&lflag, n)) || (e = dalloc(&lscan, n)) || (e = dalloc(&tiles, nt + kScanTile)) ||
             (e = dalloc(&nodes, cap)) || (e = dalloc(&splitting, cap)) || (e = dalloc(&lists, cap)) ||
-            (e = dalloc(&split_flag, n)) || (e = dalloc(&split_rank, n)) || (e = dalloc(&size, cap)))
+            (e = dalloc(&split_flag, n)) || (e = dalloc(&split_rank, n)) || (e = dalloc(&size, cap)) ||
+            (e = dalloc(&need, n)) || (e = dalloc(&need_rank, n)))
             break;
+        // fixed temporaries (the bins and the layout positions are added below)
+        size_t temp = (size_t)n * (9 * sizeof(float) + 10 * sizeof(uint32_t)) +
+                      (size_t)cap * (sizeof(GNode) + 1 + 2 * sizeof(uint32_t)) + (nt + kScanTile) * sizeof(uint32_t);
         // root: node 0 = every triangle
         GNode root{};
         for (int a = 0; a < 3; ++a) {
@@ -561,19 +592,37 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
             level_off.push_back(list_off);
             level_cnt.push_back(m);
             const uint32_t* active = lists + list_off;
-            if ((size_t)m * kSlotWords > bins_cap) {
+            // bin slots only for the nodes that can split (a node of one
+            // triangle becomes a leaf without reading bins), at most
+            // kMaxBinSlots at a time: the level runs in batches of slots
+            hipLaunchKernelGGL(need_bins_kernel, grid1(m), dim3(256), 0, s, m, active, nodes, need);
+            if ((e = scan_u32(need, need_rank, m, tiles, s))) break;
+            uint32_t nlast[2];
+            if ((e = hipMemcpyAsync(&nlast[0], need_rank + m - 1, 4, hipMemcpyDeviceToHost, s)) ||
+                (e = hipMemcpyAsync(&nlast[1], need + m - 1, 4, hipMemcpyDeviceToHost, s)) ||
+                (e = hipStreamSynchronize(s)))
+                break;
+            const uint32_t nneed = nlast[0] + nlast[1];
+            const uint32_t slots = nneed < kMaxBinSlots ? nneed : kMaxBinSlots;
+            if ((size_t)slots * kSlotWords > bins_cap) {
                 (void)hipFree(bins);
                 bins = nullptr;
-                bins_cap = (size_t)m * kSlotWords * 2;
+                bins_cap = (size_t)slots * kSlotWords;
                 if ((e = hipMalloc((void**)&bins, bins_cap * sizeof(uint32_t)))) break;
+                if (bins_cap * sizeof(uint32_t) > bins_peak) bins_peak = bins_cap * sizeof(uint32_t);
             }
-            // bins: counts 0, lo = +inf (0xFFFFFFFF), hi = -inf (0)
-            hipLaunchKernelGGL(clear_bins_kernel, grid1(m * kSlotWords), dim3(256), 0, s, bins, m);
-            hipLaunchKernelGGL(assign_slots_kernel, grid1(m), dim3(256), 0, s, m, active, nodes);
-            hipLaunchKernelGGL(bin_chunk_kernel, dim3((n + kBinChunk - 1) / kBinChunk), dim3(kBinThreads), 0, s,
-                               n, ids, seg, nodes, bl, bh, cen, bins);
-            hipLaunchKernelGGL(split_kernel, grid1(m, 64), dim3(64), 0, s, m, active, nodes, bins, leaf_max,
-                               trav_cost, margin, split_flag);
+            for (uint32_t b0 = 0; b0 == 0 || b0 < nneed; b0 += kMaxBinSlots) {
+                const uint32_t nb = nneed - b0 < kMaxBinSlots ? nneed - b0 : kMaxBinSlots;
+                // bins: counts 0, lo = +inf (0xFFFFFFFF), hi = -inf (0)
+                if (nb) hipLaunchKernelGGL(clear_bins_kernel, grid1(nb * kSlotWords), dim3(256), 0, s, bins, nb);
+                hipLaunchKernelGGL(assign_slots_kernel, grid1(m), dim3(256), 0, s, m, active, need, need_rank, b0, nb,
+                                   nodes);
+                if (nb)
+                    hipLaunchKernelGGL(bin_chunk_kernel, dim3((n + kBinChunk - 1) / kBinChunk), dim3(kBinThreads), 0,
+                                       s, n, ids, seg, nodes, bl, bh, cen, bins);
+                hipLaunchKernelGGL(split_kernel, grid1(m, 64), dim3(64), 0, s, m, active, nodes, bins, leaf_max,
+                                   trav_cost, margin, split_flag, b0 == 0 ? 1u : 0u);
+            }
             if ((e = scan_u32(split_flag, split_rank, m, tiles, s))) break;
             hipLaunchKernelGGL(mark_kernel, grid1(m), dim3(256), 0, s, m, active, split_flag, splitting);
             hipLaunchKernelGGL(left_flag_kernel, grid1(n), dim3(256), 0, s, n, ids, seg, nodes, splitting, cen, lflag);
@@ -605,6 +654,8 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
             hipLaunchKernelGGL(size_kernel, grid1(level_cnt[L]), dim3(256), 0, s, level_cnt[L], lists + level_off[L],
                                nodes, size);
         if ((e = dalloc(&pos, 8 * (size_t)cap))) break;
+        temp += 8 * (size_t)cap * sizeof(uint32_t);
+        if (temp_bytes) *temp_bytes = temp + bins_peak;
         if ((e = hipMemsetAsync(pos, 0, 8 * (size_t)cap * 4, s))) break;  // the root at 0 in every layout
         for (size_t L = 0; L < level_cnt.size(); ++L)
             hipLaunchKernelGGL(pos_kernel, dim3((level_cnt[L] + 255) / 256, 8), dim3(256), 0, s, level_cnt[L],
@@ -634,6 +685,8 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
     (void)hipFree(pos);
     (void)hipFree(splitting);
     (void)hipFree(nodes);
+    (void)hipFree(need);
+    (void)hipFree(need_rank);
     return e;
 }
 

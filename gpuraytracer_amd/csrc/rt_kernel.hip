@@ -1099,7 +1099,15 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
 
 
 hipError_t read_debug_stats(unsigned long long* out, int n) {
-#ifdef RT_STATS
+#if defined(RT_FREE_DEBUG)
+    // the free kernel's event log (rt_free.hpp), as 64-bit words
+    constexpr int kWords = (int)(sizeof(g_free_dbg) / 8);
+    if (n > kWords) n = kWords;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_free_dbg), n * sizeof(unsigned long long));
+    if (e != hipSuccess) return e;
+    static const uint32_t zero[4] = {0, 0, 0, 0};  // the three slot counters
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_free_dbg), zero, sizeof(zero));
+#elif defined(RT_STATS)
     if (n > 32) n = 32;
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stats), n * sizeof(unsigned long long));
     if (e != hipSuccess) return e;

@@ -69,6 +69,7 @@ struct KParams {
     uint32_t lanes;           // lanes per pixel: 0 = auto, else 1, 4 or 16 (rt_create_options)
     uint32_t walk;            // rt_walk_scheduler: 0 auto, 1 lockstep, 2 free-running lanes, 3 sorted
     uint32_t wave_w;          // pixels per wave row (set by the launcher)
+    uint32_t walk_leaf_den;   // free-running walks: leaf-round threshold, 0 = default
     const float4* clusters;   // box clusters, kCluF4 float4 each, or null
     uint32_t nC;              // clusters (0: none)
     uint32_t pair_free;       // pairs in no cluster (bit mask)
@@ -125,10 +126,11 @@ hipError_t build_tri_lbvh(const float4* d_tri, uint32_t n, const float lo[3], co
 // GPU binned-SAH build of the triangle BVH (rt_gsah.hip): the host build's
 // rules (32 bins, SAH leaf rule) level by level on the device, written in the
 // same compact layout.  d_nodes: 8 * (2n-1) uint4 at most, d_sorted: 3n
-// float4, d_perm: n; *total_nodes = nodes per layout.  Synchronises the stream.
+// float4, d_perm: n; *total_nodes = nodes per layout, *temp_bytes = the peak
+// of the build's temporary device memory.  Synchronises the stream.
 hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_t leaf_max, double trav_cost,
                           uint4* d_nodes, float4* d_sorted, uint32_t* d_perm, uint32_t* total_nodes,
-                          hipStream_t s);
+                          size_t* temp_bytes, hipStream_t s);
 // Deterministic exclusive scan of n uint32 (rt_gsah.hip); tile_sums holds
 // ceil(n / 1024) words.
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tile_sums, hipStream_t s);

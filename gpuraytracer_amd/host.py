@@ -95,7 +95,8 @@ class Options:
     none changes a rendered value.  Defaults are the library's measured best.
     ``layout`` in ``LAYOUTS`` (auto, pairs, single, global, pairsmem, sorted,
     bvh), ``tri_build`` in ``TRI_BUILDS`` (default, host, lbvh, gpusah),
-    ``walk`` in ``WALKS`` (auto, lockstep, free)."""
+    ``walk`` in ``WALKS`` (auto, lockstep, free, sorted);
+    ``walk_leaf_den`` the free scheduler's leaf-round threshold (0 = default)."""
 
     layout: str = "auto"
     lanes: int = 0
@@ -105,6 +106,7 @@ class Options:
     sphere_leaf_max: int = 0
     sphere_median: bool = False
     walk: str = "auto"
+    walk_leaf_den: int = 0
 
     def c(self) -> CreateOptions:
         o = CreateOptions()
@@ -116,6 +118,7 @@ class Options:
         o.sphere_leaf_max = self.sphere_leaf_max
         o.sphere_median = 1 if self.sphere_median else 0
         o.walk_scheduler = WALKS[self.walk]
+        o.walk_leaf_den = self.walk_leaf_den
         return o
 
     # tools and the bench take their A/B knobs from the environment; the
@@ -264,7 +267,10 @@ class Scene:
         return cls(base.camera, mats, verts, base.light)
 
     def describe(self, options: Options | None = None) -> dict:
-        """Device layout rt_create would choose (rt_scene_describe_ex)."""
+        """Device layout rt_create would choose (rt_scene_describe_ex).  It
+        describes the lockstep kernels: with ``walk`` free or sorted a BVH
+        scene runs another kernel (``Renderer.last_launch()`` names it and its
+        LDS bytes)."""
         info = SceneInfo()
         opt = None if options is None else ctypes.byref(options.c())
         _check(lib.rt_scene_describe_ex(ctypes.byref(self.desc()), opt, ctypes.byref(info)))

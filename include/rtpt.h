@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RTPT_ABI_VERSION 6
+#define RTPT_ABI_VERSION 7
 
 /* Maximum bounce count: Halton dimensions 2+5b..5+5b must stay inside the
  * 24-entry `primes[]` table (`RTrace/sampling.metal:97-104`); b <= 3. */
@@ -146,7 +146,11 @@ typedef struct rt_create_options {
     uint32_t sphere_leaf_max;  /* spheres per BVH leaf at most, 0 = 1; 1..255        */
     uint32_t sphere_median;    /* 1: median splits instead of the exact SAH sweep    */
     uint32_t walk_scheduler;   /* rt_walk_scheduler (BVH scenes)                     */
-    uint32_t reserved[8];      /* must be 0                                          */
+    uint32_t walk_leaf_den;    /* RT_WALK_FREE: parked leaves are tested once they
+                                  are >= 1/den of the walking lanes, 0 = default;
+                                  1..64 (1: only when every walker is parked, so
+                                  leaves stay parked into the service phase)       */
+    uint32_t reserved[7];      /* must be 0                                          */
 } rt_create_options;
 
 /* The defaults (all zero). */
@@ -261,13 +265,15 @@ typedef struct rt_launch_info {
 int rt_last_launch(const rt_ctx* ctx, rt_launch_info* info);
 
 /* How rt_create built the scene: which triangle-BVH build ran (rt_tri_bvh_build,
- * 0 = no triangle BVH), its nodes per octant layout, and the wall times of the
- * build (device sync / upload included) and of the host scene compile. */
+ * 0 = no triangle BVH), its nodes per octant layout, the wall times of the
+ * build (device sync / upload included) and of the host scene compile, and the
+ * peak temporary device memory of the GPU SAH build (KiB; 0 for the others). */
 typedef struct rt_build_stats {
     uint32_t tri_bvh_build;
     uint32_t tri_bvh_nodes;
     float tri_bvh_build_ms;
     float scene_compile_ms;
+    uint32_t tri_bvh_temp_kib;
 } rt_build_stats;
 int rt_build_info(const rt_ctx* ctx, rt_build_stats* info);
 
@@ -342,7 +348,9 @@ int rt_scene_cornell_box_mis(int32_t width, int32_t height, CameraGPU* camera,
                              SquareLightGPU* light, uint32_t* n_triangles);
 
 /* How rt_create would lay a scene out on the device (host-only, no device),
- * with default options; rt_scene_describe_ex with `opt` (NULL = defaults). */
+ * with default options; rt_scene_describe_ex with `opt` (NULL = defaults).
+ * It describes the lockstep kernels: with walk_scheduler FREE or SORTED a BVH
+ * scene runs another kernel, whose name and LDS bytes rt_last_launch reports. */
 typedef struct rt_scene_info {
     uint32_t n_triangles;
     uint32_t n_triangle_pairs;   /* >0: every (2k,2k+1) shares v0 and an edge -> pair records */

@@ -115,7 +115,7 @@ def test_create_options_are_validated_without_a_device():
     assert bytes(o) == bytes(ctypes.sizeof(o))  # the defaults are all zero
     for field, bad in [("scene_layout", 7), ("lanes_per_pixel", 2), ("tri_bvh_build", 9),
                        ("tri_leaf_max", 129), ("sphere_leaf_max", 256), ("sphere_median", 2),
-                       ("walk_scheduler", 4), ("tri_leaf_cost", -1.0)]:
+                       ("walk_scheduler", 4), ("walk_leaf_den", 65), ("tri_leaf_cost", -1.0)]:
         q = _native.CreateOptions()
         setattr(q, field, bad)
         assert g.lib.rt_create_ex(ctypes.byref(desc), ctypes.byref(q), ctypes.byref(ctx)) == 1, field

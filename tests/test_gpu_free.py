@@ -46,6 +46,23 @@ def test_free_spheres_1000_more_samples(walk):
     assert_parity(out, oracle_lib.render(s, sd, 9, 3), "free spheres1000")
 
 
+@pytest.mark.parametrize("den", [1, 64])
+@pytest.mark.parametrize("kind", ["spheres", "triangles"])
+def test_free_leaf_rounds_at_both_sites(kind, den):
+    """The free scheduler resolves a parked leaf in two places: in the walk
+    loop's leaf rounds and, for leaves still parked when the walk phase stops,
+    at the top of the service phase.  walk_leaf_den = 1 holds the leaf rounds
+    until every walker is parked, so most leaves reach the service site;
+    64 runs a round for almost every parked leaf.  Both bit-exact."""
+    if kind == "spheres":
+        s = Scene.random_spheres(48, 32, 1000, seed=42)
+    else:
+        s = triangle_soup(48, 32, 3000, seed=3000, dup=True)
+    sd = seed_splitmix(48, 32)
+    out = render_free(s, sd, RenderParams(spp=9, bounces=3), "free", walk_leaf_den=den)
+    assert_parity(out, oracle_lib.render(s, sd, 9, 3), f"free {kind} leaf den {den}")
+
+
 @pytest.mark.parametrize("leaf", [3, 8])
 def test_free_spheres_multi_sphere_leaves(leaf, walk):
     s = Scene.random_spheres(40, 24, 700, seed=5)

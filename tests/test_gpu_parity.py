@@ -450,6 +450,30 @@ def test_triangle_bvh_gpu_build_bit_exact(n, dup, build):
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"soup{n}")
 
 
+def test_gpu_sah_1m_triangles_bounded_temporaries():
+    """1M triangles: the GPU SAH build gives bin slots (2,688 B) only to nodes
+    that can split, at most 65,536 at a time (the deep levels run in batches),
+    so its peak temporary device memory stays ~0.5 GB (round 5: one slot per
+    node of a level, doubling: 2.7-5.4 GB).  The batched build is the host
+    SAH's tree: same node count, and the frames rendered on both trees agree
+    bit for bit (each walk returns the brute-force (t, id) answer)."""
+    n = 1_000_000
+    s = Scene.random_triangles(64, 48, n)
+    sd = seed_splitmix(64, 48)
+    p = RenderParams(spp=2, bounces=3)
+    with Renderer(s, seeds=sd, options=Options(tri_build="gpusah")) as r:
+        info = r.build_info()
+        gpu = r.render(p)
+    with Renderer(s, seeds=sd, options=Options(tri_build="host")) as r:
+        host_info = r.build_info()
+        host = r.render(p)
+    assert info["tri_bvh_build"] == 3 and host_info["tri_bvh_build"] == 1, (info, host_info)
+    assert info["tri_bvh_nodes"] == host_info["tri_bvh_nodes"] == 2 * (n + 36) - 1, (info, host_info)
+    assert 0 < info["tri_bvh_temp_kib"] * 1024 < 600e6, info
+    assert host_info["tri_bvh_temp_kib"] == 0
+    assert np.array_equal(gpu.view(np.uint32), host.view(np.uint32))
+
+
 @pytest.mark.parametrize("build", ["gpusah", "host"])
 def test_triangle_bvh_coincident_centroids(build):
     """600 copies of one small triangle (every centroid in one point: the SAH
