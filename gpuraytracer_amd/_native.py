@@ -88,7 +88,7 @@ class SceneInfo(ctypes.Structure):  # rt_scene_info
     _fields_ = [(n, ctypes.c_uint32) for n in
                 ("n_triangles", "n_triangle_pairs", "n_spheres", "lds_bytes",
                  "n_sphere_nodes", "n_triangle_bvh_nodes", "n_box_clusters", "pair_free_mask",
-                 "sphere_kernel_lds_bytes")]
+                 "sphere_kernel_lds_bytes", "kernel_layout", "kernel_lds_bytes")]
 
 
 class CreateOptions(ctypes.Structure):  # rt_create_options

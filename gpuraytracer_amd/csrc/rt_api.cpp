@@ -307,6 +307,10 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     if (sync) {
         if ((e = hipStreamSynchronize(stream)) != hipSuccess)
             return hip_fail(c, RT_ERR_LAUNCH, "path_trace execution", e);
+        uint32_t short_end = 0;  // RT_LDS_CHECK builds (rt_kernel.hip)
+        if (rt::lds_check_result(&short_end) == hipSuccess && short_end)
+            return fail(c, RT_ERR_LAUNCH, "LDS overflow: staged records end at byte " + std::to_string(short_end) +
+                                              ", past the dispatch's dynamic LDS");
     }
     return RT_OK;
 }
@@ -1016,6 +1020,12 @@ int rt_scene_describe_ex(const rt_scene_desc* d, const rt_create_options* opt, r
     info->lds_bytes = (!bvh && lds <= rt::kMaxLdsBytes)
                           ? (uint32_t)(lds_clu <= rt::kMaxLdsBytes ? lds_clu : lds)
                           : 0u;
+    // the launcher's own choice (rt::choose_kernel), for a render of >= 1 bounce
+    const rt::KernelChoice kc =
+        rt::choose_kernel(info->n_triangles, info->n_triangle_pairs, info->n_spheres, info->n_box_clusters,
+                          info->n_triangle_bvh_nodes, !s.sph_lds.empty(), 3, ro.mem, ro.walk);
+    info->kernel_layout = (uint32_t)kc.layout;
+    info->kernel_lds_bytes = (uint32_t)kc.lds_bytes;
     return RT_OK;
 }
 

@@ -177,6 +177,7 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
     sv.htab = nullptr;
     if (SPH) {  // the room's pair records in LDS; the compact sphere BVH stays in L2
         const uint32_t ng4 = kPairF4 * sv.nP;
+        RT_LDS_GUARD(16 * (size_t)ng4);
         for (uint32_t k = threadIdx.x; k < ng4; k += kFreeThreads) lds[k] = P.pair_isect[k];
         __syncthreads();
         sv.tri = lds;
@@ -578,10 +579,14 @@ __global__ __launch_bounds__(kFreeThreads, kFreeWavesPerEu) void path_free_kerne
 #endif
                 if constexpr (SPH) {
                     // every lane evaluates the roots, parked lanes keep the
-                    // result: the branch form (resolve_leaf under `if (parked)`)
-                    // measured 4 wrong values in 13,824 on 1000 spheres x 9 spp
-                    // (tests/test_gpu_free.py) where this select form and the
-                    // lockstep walk are bit-exact -- not understood, kept out
+                    // result.  The branch form (RT_FREE_BRANCH: resolve_leaf
+                    // under `if (parked)`, as the service phase does) is
+                    // bit-exact too (round 6, profiles/r6/free_walk/: the 42
+                    // free-scheduler GPU tests, and RT_FREE_CHECK re-evaluated
+                    // 43,523 walk-loop resolves of the failing round-5 case in
+                    // this form before the branch: 0 disagreements).  Round
+                    // 5's 4 wrong values came from an uncommitted intermediate
+                    // kernel, not from either form.
                     const float sq = sqrtf(parked ? pdisc : 1.0f);
                     const float a2 = 2.0f * a;
                     float t = (-pb - sq) / a2;

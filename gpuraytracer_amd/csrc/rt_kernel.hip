@@ -20,13 +20,44 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 
+#include <stddef.h>
 #include <stdio.h>
+#ifdef RT_LDS_CHECK
+#include <hsa/hsa.h>
+#endif
 
 #include "rt_kernel.hpp"
 #include "rt_halton.hpp"
 #include "rt_trace.hpp"
 
 namespace rt {
+
+// -DRT_LDS_CHECK diagnostic builds: before staging, every kernel checks that
+// the end of what its staging loops write (computed from the kernel's own
+// loop bounds) lies within the dynamic LDS of its dispatch
+// (hsa_kernel_dispatch_packet_t.group_segment_size, byte 28 = static +
+// dynamic LDS).  A short allocation records the end in g_lds_overflow and the
+// workgroup returns before writing anything; rt_render then fails with
+// RT_ERR_LAUNCH (lds_check_result).  Production builds compile it out: the
+// launcher requests staged_lds_bytes (rt_kernel.hpp), the same terms.
+#ifdef RT_LDS_CHECK
+__device__ uint32_t g_lds_overflow;
+__device__ __forceinline__ bool lds_short(size_t end) {
+    // word 7 (byte 28) of the AQL packet: group_segment_size (static_assert below)
+    const uint32_t grp = ((const uint32_t*)__builtin_amdgcn_dispatch_ptr())[7];
+    const size_t dyn = grp - __builtin_amdgcn_groupstaticsize();
+    if (end <= dyn) return false;
+    if (threadIdx.x == 0) atomicMax(&g_lds_overflow, (uint32_t)end);
+    return true;
+}
+static_assert(offsetof(hsa_kernel_dispatch_packet_t, group_segment_size) == 28, "AQL packet layout");
+#define RT_LDS_GUARD(end)            \
+    do {                             \
+        if (lds_short(end)) return;  \
+    } while (0)
+#else
+#define RT_LDS_GUARD(end) ((void)0)
+#endif
 
 namespace {
 
@@ -450,7 +481,6 @@ struct SortedChain<B, B, GEO, SPH, SMALL> {
                                                PathState&, uint32_t&, bool&) {}
 };
 
-size_t sorted_lds_extra_bytes() { return kSortF4 * sizeof(float4); }
 
 }  // namespace
 
@@ -502,11 +532,13 @@ void path_trace_kernel(KParams P) {
     if (GEO == kGeoPairSmem) {
         sv.tri = nullptr;
         sv.pair = P.pair_isect;
-    } else if (GEO != kGeoTriGlobal) {
+    } else if (GEO != kGeoTriGlobal && GEO != kGeoTriBvh) {
         // Stage the intersection records once per workgroup.
         constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu || GEO == kGeoSphLds;
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
+        RT_LDS_GUARD(16 * (size_t)(ng4 + (GEO == kGeoPairClu ? kCluF4 * P.nC : 0u)) +
+                     (GEO == kGeoPairClu ? 4 * (size_t)kHaltonTabFloats : 0));
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
         if (GEO == kGeoSphLds) {  // the compact sphere BVH (8 layouts) stays in global memory (L2)
             sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
@@ -732,6 +764,7 @@ void path_trace_sorted_kernel(
     sv.nC = 0;
     sv.htab = nullptr;
     const uint32_t ng4 = GEO == kGeoTriBvh ? 0u : kPairF4 * sv.nP;
+    RT_LDS_GUARD(16 * (size_t)(kSortF4 + ng4));
     float4* scene = lds + kSortF4;  // sort buffers first: compile-time offsets
     for (uint32_t k = threadIdx.x; k < ng4; k += kBlockThreads) scene[k] = P.pair_isect[k];
     sv.nN = SPH ? (GEO == kGeoSphLds ? P.nE : P.nN) : 0u;
@@ -866,11 +899,16 @@ inline int lanes_per_pixel(const KParams& P, int geo) {
     return P.spp >= 4 ? 4 : 1;
 }
 
-constexpr int kGeoPairSorted = 3;  // pair records + per-bounce octant sort of the paths
-constexpr int kGeoFreeSph = 8;     // free-running lanes, sphere scene (rt_free.hpp)
-constexpr int kGeoFreeTri = 9;     // free-running lanes, triangle BVH
-constexpr int kGeoSortSph = 10;    // octant-sorted paths, sphere scene
-constexpr int kGeoSortTri = 11;    // octant-sorted paths, triangle BVH
+constexpr int kGeoPairSorted = kLayPairSorted;
+constexpr int kGeoFreeSph = kLayFreeSph;
+constexpr int kGeoFreeTri = kLayFreeTri;
+constexpr int kGeoSortSph = kLaySortSph;
+constexpr int kGeoSortTri = kLaySortTri;
+static_assert(kGeoTriLds == kLayTriLds && kGeoPairLds == kLayPairLds && kGeoTriGlobal == kLayTriGlobal &&
+                  kGeoPairSmem == kLayPairSmem && kGeoTriBvh == kLayTriBvh && kGeoPairClu == kLayPairClu &&
+                  kGeoSphLds == kLaySphLds,
+              "rt_trace.hpp Geo == rt_kernel.hpp KernelLayout");
+static_assert(kHaltonTabLdsFloats == kHaltonTabFloats && kSortLdsF4 == kSortF4, "staged_lds_bytes terms");
 
 // The most recent launch of this thread (launch_path_trace copies it out).
 thread_local LaunchInfo g_last;
@@ -909,7 +947,7 @@ hipError_t launch_tl(const KParams& P, size_t lds_bytes, hipStream_t stream) {
         const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL, L>, lds_bytes);
         if (e != hipSuccess) return e;
     }
-    const size_t lds = (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes;
+    const size_t lds = lds_bytes;  // staged_lds_bytes of the layout
     note_launch<B, GEO, SPH, SMALL, L>("path_trace_kernel", Q, grid, block_threads(GEO), lds);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL, L>), grid, dim3(block_threads(GEO)),
                        lds, stream, Q);
@@ -929,7 +967,7 @@ hipError_t launch_t(const KParams& P, size_t lds_bytes, hipStream_t stream) {
         const hipError_t e = allow_lds((const void*)path_trace_kernel<B, GEO, SPH, SMALL>, lds_bytes);
         if (e != hipSuccess) return e;
     }
-    const size_t lds = (GEO == kGeoTriGlobal || GEO == kGeoPairSmem || GEO == kGeoTriBvh) ? 0 : lds_bytes;
+    const size_t lds = lds_bytes;  // staged_lds_bytes of the layout
     note_launch<B, GEO, SPH, SMALL, 1>("path_trace_kernel", P, grid, block_threads(GEO), lds);
     hipLaunchKernelGGL((path_trace_kernel<B, GEO, SPH, SMALL>), grid, dim3(block_threads(GEO)),
                        lds, stream, P);
@@ -964,7 +1002,7 @@ hipError_t launch_sorted_t(const KParams& P, size_t lds_bytes, hipStream_t strea
 template <int B, int GEO>
 hipError_t launch_sorted_g(const KParams& P, size_t lds_bytes, hipStream_t stream) {
     const bool small = P.max_index < kSmallIndexMax;
-    const size_t bytes = (GEO == kGeoTriBvh ? 0 : lds_bytes) + sorted_lds_extra_bytes();
+    const size_t bytes = lds_bytes;  // staged_lds_bytes: path buffers + scene records
     if constexpr (GEO == kGeoSphLds)
         return small ? launch_sorted_t<B, GEO, true, true>(P, bytes, stream)
                      : launch_sorted_t<B, GEO, true, false>(P, bytes, stream);
@@ -986,7 +1024,7 @@ hipError_t launch_free_t(const KParams& P, size_t lds_bytes, hipStream_t stream)
     Q.wave_w = (P.row_step > 1) ? 64u : 8u;
     const uint32_t TY = 64u / Q.wave_w;
     const dim3 grid((P.W + Q.wave_w - 1) / Q.wave_w, (P.row_count + TY - 1) / TY);
-    const size_t lds = GEO == kGeoSphLds ? lds_bytes : 0;
+    const size_t lds = lds_bytes;  // staged_lds_bytes of the layout
     note_launch<B, GEO, GEO == kGeoSphLds, SMALL, 1>("path_free_kernel", Q, grid, kFreeThreads, lds);
     hipLaunchKernelGGL((path_free_kernel<B, GEO, SMALL>), grid, dim3(kFreeThreads), lds, stream, Q);
     return hipGetLastError();
@@ -1025,66 +1063,74 @@ hipError_t launch_b(const KParams& P, int geo, size_t lds_bytes, hipStream_t str
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes) {
     (void)n_sph;  // sphere BVH nodes and records stay in global memory (scalar loads)
     (void)n_nodes;
-    const uint32_t geo4 = n_pairs ? kPairF4 * n_pairs : 3u * n_tri;
-    return (size_t)geo4 * sizeof(float4);
+    return n_pairs ? staged_lds_bytes(kLayPairLds, n_tri, n_pairs, 0) : staged_lds_bytes(kLayTriLds, n_tri, 0, 0);
+}
+
+KernelChoice choose_kernel(uint32_t nT, uint32_t nP, uint32_t nS, uint32_t nC, uint32_t nTN, bool sph_compact,
+                           uint32_t bounces, SceneMem mem, uint32_t walk) {
+    auto lds = [&](int lay) { return staged_lds_bytes(lay, nT, nP, nC); };
+    const bool pairs = nP > 0 && mem != SceneMem::kLdsSingle;
+    int geo = kGeoTriGlobal;
+    if (mem != SceneMem::kSmem && lds(pairs ? kGeoPairLds : kGeoTriLds) <= kMaxLdsBytes)
+        geo = pairs ? kGeoPairLds : kGeoTriLds;
+    if (mem == SceneMem::kPairSmem && nP > 0) geo = kGeoPairSmem;
+    // triangle BVH whenever rt_create built one (kTriBvhMinTriangles or no LDS fit),
+    // unless another layout is forced
+    if (nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) geo = kGeoTriBvh;
+    // the sphere kernel (one-wave workgroups, compact BVH in L2) while its
+    // per-workgroup copy of the pair records is small (rt_kernel.hpp)
+    if (geo == kGeoPairLds && nS > 0 && sph_compact && mem == SceneMem::kAuto &&
+        lds(kGeoSphLds) <= kSphPairLdsMaxBytes)
+        geo = kGeoSphLds;
+    // box clusters whenever rt_create found some (DESIGN.md §3.12); not with
+    // spheres, where the sphere walks dominate and the cluster code's register
+    // pressure measured 4.6 % slower than the culled pair loop (config 4)
+    if (geo == kGeoPairLds && nC > 0 && nS == 0 && mem == SceneMem::kAuto && lds(kGeoPairClu) <= kMaxLdsBytes)
+        geo = kGeoPairClu;
+    // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the
+    // Cornell 1080p workload (barrier + occupancy cost; DESIGN.md §5).
+    if (geo == kGeoPairLds && mem == SceneMem::kPairSorted && lds(kGeoPairSorted) <= kMaxLdsBytes)
+        geo = kGeoPairSorted;
+    // the free-running kernel for BVH scenes (rt_create_options.walk_scheduler)
+    if (bounces >= 1 && walk == kWalkFree) {
+        if (geo == kGeoSphLds) geo = kGeoFreeSph;
+        if (geo == kGeoTriBvh && nS == 0) geo = kGeoFreeTri;
+    }
+    // octant-sorted paths for BVH scenes (rt_create_options.walk_scheduler)
+    if (walk == kWalkSorted) {
+        if (geo == kGeoSphLds) geo = kGeoSortSph;
+        if (geo == kGeoTriBvh && nS == 0) geo = kGeoSortTri;
+    }
+    return KernelChoice{geo, lds(geo)};
 }
 
 namespace {
 hipError_t launch_path_trace_impl(const KParams& P, uint32_t bounces, SceneMem mem,
                                   hipStream_t stream) {
-    const bool pairs = P.nP > 0 && mem != SceneMem::kLdsSingle;
-    const size_t lds_bytes = kernel_lds_bytes(P.nT, pairs ? P.nP : 0u, P.nS, P.nN);
-    int geo = kGeoTriGlobal;
-    if (mem != SceneMem::kSmem && lds_bytes <= kMaxLdsBytes) geo = pairs ? kGeoPairLds : kGeoTriLds;
-    if (mem == SceneMem::kPairSmem && P.nP > 0) geo = kGeoPairSmem;
-    // triangle BVH whenever rt_create built one (kTriBvhMinTriangles or no LDS fit),
-    // unless another layout is forced
-    if (P.nTN > 0 && (mem == SceneMem::kTriBvh || mem == SceneMem::kAuto)) geo = kGeoTriBvh;
-    size_t lds_total = lds_bytes;
-    // the sphere kernel (one-wave workgroups, compact BVH in L2) while its
-    // per-workgroup copy of the pair records is small (rt_kernel.hpp)
-    if (geo == kGeoPairLds && P.nS > 0 && P.sph_lds && mem == SceneMem::kAuto &&
-        lds_bytes <= kSphPairLdsMaxBytes)
-        geo = kGeoSphLds;
-    // box clusters whenever rt_create found some (DESIGN.md §3.12); not with
-    // spheres, where the sphere walks dominate and the cluster code's register
-    // pressure measured 4.6 % slower than the culled pair loop (config 4)
-    if (geo == kGeoPairLds && P.nC > 0 && P.nS == 0 && mem == SceneMem::kAuto &&
-        lds_bytes + kCluF4 * P.nC * sizeof(float4) + kHaltonTabFloats * sizeof(float) <= kMaxLdsBytes) {
-        geo = kGeoPairClu;
-        lds_total = lds_bytes + kCluF4 * P.nC * sizeof(float4) + kHaltonTabFloats * sizeof(float);
-    }
-    // Opt-in only: bit-identical, 31% fewer pair tests, but 18% slower on the
-    // Cornell 1080p workload (barrier + occupancy cost; DESIGN.md §5).
-    if (geo == kGeoPairLds && mem == SceneMem::kPairSorted &&
-        lds_bytes + sorted_lds_extra_bytes() <= kMaxLdsBytes)
-        geo = kGeoPairSorted;
-    // the free-running kernel for BVH scenes (rt_create_options.walk_scheduler)
-    if (bounces >= 1 && P.walk == kWalkFree) {
-        if (geo == kGeoSphLds) geo = kGeoFreeSph;
-        if (geo == kGeoTriBvh && P.nS == 0) geo = kGeoFreeTri;
-    }
-    // octant-sorted paths for BVH scenes (rt_create_options.walk_scheduler)
-    if (P.walk == kWalkSorted) {
-        if (geo == kGeoSphLds) geo = kGeoSortSph;
-        if (geo == kGeoTriBvh && P.nS == 0) geo = kGeoSortTri;
-    }
+    const KernelChoice kc = choose_kernel(P.nT, P.nP, P.nS, P.nC, P.nTN, P.sph_lds != nullptr, bounces, mem, P.walk);
+    const int geo = kc.layout;
+    const size_t lds_total = kc.lds_bytes;  // exactly what the layout's staging loops write
+#ifdef RT_LDS_UNDERSIZE  // negative control of the RT_LDS_CHECK build: one float4 short
+    const size_t lds_req = lds_total >= 16 ? lds_total - 16 : lds_total;
+#else
+    const size_t lds_req = lds_total;
+#endif
 #ifdef RT_DEV_ISA  // ISA-inspection builds only (tools/isa.sh): the two headline layouts at B = 3
     if (bounces != 3) return hipErrorInvalidValue;
-    if (geo == kGeoFreeSph) return launch_free<3, kGeoSphLds>(P, lds_total, stream);
-    if (geo == kGeoFreeTri) return launch_free<3, kGeoTriBvh>(P, lds_total, stream);
-    if (geo == kGeoSortSph) return launch_sorted_g<3, kGeoSphLds>(P, lds_total, stream);
-    if (geo == kGeoSortTri) return launch_sorted_g<3, kGeoTriBvh>(P, lds_total, stream);
-    if (geo == kGeoTriBvh) return launch_g<3, kGeoTriBvh>(P, lds_total, stream);
-    return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_total, stream)
-                              : launch_g<3, kGeoSphLds>(P, lds_total, stream);
+    if (geo == kGeoFreeSph) return launch_free<3, kGeoSphLds>(P, lds_req, stream);
+    if (geo == kGeoFreeTri) return launch_free<3, kGeoTriBvh>(P, lds_req, stream);
+    if (geo == kGeoSortSph) return launch_sorted_g<3, kGeoSphLds>(P, lds_req, stream);
+    if (geo == kGeoSortTri) return launch_sorted_g<3, kGeoTriBvh>(P, lds_req, stream);
+    if (geo == kGeoTriBvh) return launch_g<3, kGeoTriBvh>(P, lds_req, stream);
+    return geo == kGeoPairClu ? launch_g<3, kGeoPairClu>(P, lds_req, stream)
+                              : launch_g<3, kGeoSphLds>(P, lds_req, stream);
 #endif
     switch (bounces) {
-        case 0: return launch_b<0>(P, geo, lds_total, stream);
-        case 1: return launch_b<1>(P, geo, lds_total, stream);
-        case 2: return launch_b<2>(P, geo, lds_total, stream);
-        case 3: return launch_b<3>(P, geo, lds_total, stream);
-        case 4: return launch_b<4>(P, geo, lds_total, stream);
+        case 0: return launch_b<0>(P, geo, lds_req, stream);
+        case 1: return launch_b<1>(P, geo, lds_req, stream);
+        case 2: return launch_b<2>(P, geo, lds_req, stream);
+        case 3: return launch_b<3>(P, geo, lds_req, stream);
+        case 4: return launch_b<4>(P, geo, lds_req, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1097,6 +1143,18 @@ hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem,
     return e;
 }
 
+
+hipError_t lds_check_result(uint32_t* end) {
+    *end = 0;
+#ifdef RT_LDS_CHECK
+    hipError_t e = hipMemcpyFromSymbol(end, HIP_SYMBOL(g_lds_overflow), sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    const uint32_t zero = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_lds_overflow), &zero, sizeof(zero));
+#else
+    return hipSuccess;
+#endif
+}
 
 hipError_t read_debug_stats(unsigned long long* out, int n) {
 #if defined(RT_FREE_DEBUG)

@@ -76,6 +76,47 @@ struct KParams {
 };
 
 size_t kernel_lds_bytes(uint32_t n_tri, uint32_t n_pairs, uint32_t n_sph, uint32_t n_nodes);
+
+// Kernel layouts the launcher chooses between (0-7 = rt_trace.hpp enum Geo).
+enum KernelLayout : int {
+    kLayTriLds = 0,      // single-triangle records in LDS
+    kLayPairLds = 1,     // shared-edge pair records in LDS
+    kLayTriGlobal = 2,   // single-triangle records from global memory
+    kLayPairSorted = 3,  // pair records + per-bounce octant sort of the paths
+    kLayPairSmem = 4,    // pair records by scalar loads
+    kLayTriBvh = 5,      // triangle BVH from global memory
+    kLayPairClu = 6,     // pair records + box clusters + Halton tables in LDS (Cornell)
+    kLaySphLds = 7,      // pair records in LDS, compact sphere BVH in L2 (config 4)
+    kLayFreeSph = 8,     // free-running lanes, sphere scene (rt_free.hpp)
+    kLayFreeTri = 9,     // free-running lanes, triangle BVH
+    kLaySortSph = 10,    // octant-sorted paths, sphere scene
+    kLaySortTri = 11,    // octant-sorted paths, triangle BVH
+};
+// LDS of the Halton low-digit tables (rt_halton.hpp kHaltonTabFloats) and of
+// the sorted kernel's path buffers (rt_kernel.hip kSortF4), static-asserted
+// against their definitions.
+constexpr uint32_t kHaltonTabLdsFloats = 4679;
+constexpr uint32_t kSortLdsF4 = 1097;
+// THE dynamic LDS of a workgroup of layout `lay`: the bytes its staging loops
+// write (pair / triangle records, then box clusters, then the Halton tables;
+// the sorted kernels' path buffers first).  The launcher requests exactly this
+// and the kernels place their staged arrays by the same terms; an
+// -DRT_LDS_CHECK build also checks it against the dispatch's LDS allocation.
+__host__ __device__ constexpr size_t staged_lds_bytes(int lay, uint32_t nT, uint32_t nP, uint32_t nC) {
+    return lay == kLayTriLds ? (size_t)48 * nT
+           : (lay == kLayPairLds || lay == kLaySphLds || lay == kLayFreeSph) ? (size_t)16 * kPairF4 * nP
+           : lay == kLayPairClu ? (size_t)16 * (kPairF4 * nP + kCluF4 * nC) + (size_t)4 * kHaltonTabLdsFloats
+           : (lay == kLayPairSorted || lay == kLaySortSph) ? (size_t)16 * (kSortLdsF4 + kPairF4 * nP)
+           : lay == kLaySortTri ? (size_t)16 * kSortLdsF4
+           : (size_t)0;  // TriGlobal, PairSmem, TriBvh, FreeTri: the scene stays in global memory
+}
+// The kernel layout a launch takes and its dynamic LDS (launch_path_trace and
+// rt_scene_describe_ex both ask this one function).  nC: box clusters, nTN:
+// triangle-BVH nodes per layout, sph_compact: the compact sphere BVH exists.
+struct KernelChoice {
+    int layout;
+    size_t lds_bytes;
+};
 // What launch_path_trace launched (rt_last_launch, include/rtpt.h).
 struct LaunchInfo {
     char kernel[96];
@@ -87,7 +128,12 @@ constexpr uint32_t kWalkAuto = 0, kWalkLockstep = 1, kWalkFree = 2, kWalkSorted 
 enum class SceneMem { kAuto = 0, kLdsSingle = 1, kSmem = 2, kPairSorted = 3, kPairSmem = 4, kTriBvh = 5, kPairLds = 6 };
 hipError_t launch_path_trace(const KParams& P, uint32_t bounces, SceneMem mem, hipStream_t stream,
                              LaunchInfo* info);
+KernelChoice choose_kernel(uint32_t nT, uint32_t nP, uint32_t nS, uint32_t nC, uint32_t nTN, bool sph_compact,
+                           uint32_t bounces, SceneMem mem, uint32_t walk);
 hipError_t read_debug_stats(unsigned long long* out, int n);  // RT_STATS builds only
+// -DRT_LDS_CHECK builds: the largest staging end a kernel found past its
+// dispatch's dynamic LDS since the last call (0: none; always 0 otherwise).
+hipError_t lds_check_result(uint32_t* end);
 // Arguments of the MIS integrator kernel (rt_mis.hip; Sources/gpuRaytracer/
 // shaders.metal:635-707).
 struct MisParams {

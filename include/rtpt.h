@@ -363,6 +363,13 @@ typedef struct rt_scene_info {
     uint32_t n_box_clusters;     /* pair runs on the faces of one oriented box (slab-tested first) */
     uint32_t pair_free_mask;     /* pairs in no box cluster (bit k = pair k) */
     uint32_t sphere_kernel_lds_bytes; /* dynamic LDS of the sphere kernel (its pair records; 0: sphere kernel not taken) */
+    uint32_t kernel_layout;      /* the kernel layout a render (bounces >= 1) takes with these
+                                    options (rt_kernel.hpp KernelLayout: 0 triangles in LDS,
+                                    1 pairs, 2 global, 3 sorted pairs, 4 pairs by scalar loads,
+                                    5 triangle BVH, 6 pairs + box clusters, 7 sphere kernel,
+                                    8/9 free-running, 10/11 sorted BVH walks) */
+    uint32_t kernel_lds_bytes;   /* that kernel's dynamic LDS per workgroup: exactly what its
+                                    staging loops write (rt_last_launch reports the same) */
 } rt_scene_info;
 int rt_scene_describe(const rt_scene_desc* scene, rt_scene_info* info);
 int rt_scene_describe_ex(const rt_scene_desc* scene, const rt_create_options* opt, rt_scene_info* info);

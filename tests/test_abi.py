@@ -80,7 +80,8 @@ def test_scene_layout_uses_shared_edge_pairs():
     # four box clusters: the room (5 walls), the two rotated boxes, the light rectangle
     assert info == {"n_triangles": 36, "n_triangle_pairs": 18, "n_spheres": 0,
                     "lds_bytes": 18 * 112 + 4 * 112, "n_sphere_nodes": 0, "n_triangle_bvh_nodes": 0,
-                    "n_box_clusters": 4, "pair_free_mask": 0, "sphere_kernel_lds_bytes": 0}
+                    "n_box_clusters": 4, "pair_free_mask": 0, "sphere_kernel_lds_bytes": 0,
+                    "kernel_layout": 6, "kernel_lds_bytes": 18 * 112 + 4 * 112 + 4 * 4679}
     boxes = g.Scene.random_boxes(16, 8, 4, seed=1).describe()
     assert boxes["n_box_clusters"] == 6 and boxes["pair_free_mask"] == 0  # room, 4 boxes, light
     soup = g.Scene.random_triangles(16, 8, 1000).describe()
@@ -103,6 +104,45 @@ def test_scene_layout_uses_shared_edge_pairs():
     big = g.Scene.random_spheres(16, 8, 5000).describe()
     assert big["lds_bytes"] == 6 * 112 and big["sphere_kernel_lds_bytes"] == 6 * 112
     assert big["n_sphere_nodes"] == bvh_nodes(5000)
+
+
+# (scene, options) -> (kernel layout, dynamic LDS bytes the launcher requests):
+# the bytes each layout's staging loops write, restated here from the kernels
+# (rt_kernel.hip path_trace_kernel / path_trace_sorted_kernel, rt_free.hpp):
+# pair records 112 B, single triangles 48 B, box clusters 112 B, Halton tables
+# 4,679 floats, the sorted kernels' path buffers 1,097 float4 first.
+PAIR, TRI, CLU, TAB, SORT = 112, 48, 112, 4 * 4679, 16 * 1097
+LAYOUT_CASES = [
+    ("cornell", {}, 6, 18 * PAIR + 4 * CLU + TAB),
+    ("cornell", {"layout": "pairs"}, 1, 18 * PAIR),
+    ("cornell", {"layout": "single"}, 0, 36 * TRI),
+    ("cornell", {"layout": "global"}, 2, 0),
+    ("cornell", {"layout": "pairsmem"}, 4, 0),
+    ("cornell", {"layout": "sorted"}, 3, SORT + 18 * PAIR),
+    ("cornell", {"layout": "bvh"}, 5, 0),
+    ("spheres", {}, 7, 6 * PAIR),
+    ("spheres", {"walk": "free"}, 8, 6 * PAIR),
+    ("spheres", {"walk": "sorted"}, 10, SORT + 6 * PAIR),
+    ("soup", {}, 5, 0),
+    ("soup", {"walk": "free"}, 9, 0),
+    ("soup", {"walk": "sorted"}, 11, SORT),
+]
+
+
+def layout_scene(name):
+    return {"cornell": lambda: g.Scene.cornell_box(48, 32),
+            "spheres": lambda: g.Scene.random_spheres(48, 32, 300, seed=3),
+            "soup": lambda: g.Scene.random_triangles(48, 32, 1000)}[name]()
+
+
+@pytest.mark.parametrize("name,opt,layout,lds", LAYOUT_CASES)
+def test_kernel_layout_and_staged_lds_per_layout(name, opt, layout, lds):
+    """rt_scene_describe_ex reports the launcher's own choice (rt::choose_kernel)
+    and the dynamic LDS it requests, staged_lds_bytes: equal to what that
+    layout's staging loops write (tests/test_gpu_parity.py checks
+    rt_last_launch against it on the GPU)."""
+    info = layout_scene(name).describe(g.Options(**opt))
+    assert (info["kernel_layout"], info["kernel_lds_bytes"]) == (layout, lds), info
 
 
 def test_create_options_are_validated_without_a_device():

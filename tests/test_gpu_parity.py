@@ -552,3 +552,22 @@ def test_zero_light_terms_black_materials_bit_exact(mem):
         out = r.render(RenderParams(spp=4, bounces=3))
     assert_parity(out, oracle_lib.render(scene, sd, 4, 3), f"black materials {mem}")
     assert np.isfinite(out).all()
+
+
+@pytest.mark.parametrize("case", range(13))
+def test_launch_lds_equals_staged_bytes_per_layout(case):
+    """Every kernel layout: the launch requests exactly the dynamic LDS
+    rt_scene_describe_ex reports (staged_lds_bytes: what its staging loops
+    write) and renders bit-exact.  tests/test_abi.py restates the bytes per
+    layout on the CPU; an -DRT_LDS_CHECK build also checks them inside the
+    kernels against the dispatch's LDS."""
+    from test_abi import LAYOUT_CASES, layout_scene
+    name, opt, layout, lds = LAYOUT_CASES[case]
+    s = layout_scene(name)
+    assert s.describe(Options(**opt))["kernel_lds_bytes"] == lds
+    sd = seed_splitmix(48, 32)
+    with Renderer(s, seeds=sd, options=Options(**opt)) as r:
+        out = r.render(RenderParams(spp=2, bounces=3))
+        info = r.last_launch()
+    assert info["lds_bytes"] == lds, (info, layout)
+    assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"layout {layout}")
