@@ -61,6 +61,31 @@ static_assert(offsetof(hsa_kernel_dispatch_packet_t, group_segment_size) == 28, 
 
 namespace {
 
+// -DRT_CENSUS=k: VALU census builds of the box-cluster (Cornell) kernel
+// (tools/census.sh).  Build k runs phase k a second time on opaque copies of
+// its inputs (the compiler cannot reuse the first result) and discards the
+// result through an opaque sink, under the same lanes and control flow: the
+// SQ_INSTS_VALU difference to the plain build is the phase's dynamic VALU.
+// 1 camera ray (Halton dims 0-1 + generateCameraRay), 2 closest-hit queries,
+// 3 shadow queries, 4 Halton dims 2-5 of the bounces, 5 the rest of the
+// shading arithmetic (light sample, NEE term, cosine direction), 6 the
+// in-order pixel sums.  Timing-invalid by construction; never shipped.
+#ifndef RT_CENSUS
+#define RT_CENSUS 0
+#endif
+template <typename T>
+__device__ __forceinline__ T cz(T v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ f3 cz(f3 v) { return f3{cz(v.x), cz(v.y), cz(v.z)}; }
+__device__ __forceinline__ void cz_sink(float v) { asm volatile("" ::"v"(v)); }
+__device__ __forceinline__ void cz_sink(f3 v) {
+    cz_sink(v.x);
+    cz_sink(v.y);
+    cz_sink(v.z);
+}
+
 struct PathState {
     f3 o, d, acc, thr;
     uint32_t i;  // Halton index seed + n
@@ -107,9 +132,46 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     }
     f3 p = (s.o + s.d * t) + N * 1e-3f;              // :67
 
+#if RT_CENSUS == 4
+    {
+        const uint32_t i2 = cz(s.i);
+        float h = halton_dim<2 + 5 * b, SMALL, GEO == kGeoPairClu>(i2, sv.htab) +
+                  halton_dim<3 + 5 * b, SMALL, GEO == kGeoPairClu>(i2, sv.htab);
+        if (b + 1 < B)
+            h = h + halton_dim<4 + 5 * b, SMALL, GEO == kGeoPairClu>(i2, sv.htab) +
+                halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(i2, sv.htab);
+        cz_sink(h);
+    }
+#endif
     // sampleAreaLight (sampling.metal:198-236), dims 2+5b, 3+5b (:72-74)
     const float ux = halton_dim<2 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab) * 2.0f - 1.0f;
     const float uy = halton_dim<3 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab) * 2.0f - 1.0f;
+#if RT_CENSUS == 5
+    {
+        const f3 o2 = cz(s.o), dd = cz(s.d), N2 = cz(N), r2 = cz(right), f2 = cz(fwd), df = cz(diffuse);
+        const float t2 = cz(t), ux2 = cz(ux), uy2 = cz(uy);
+        const f3 p2 = (o2 + dd * t2) + N2 * 1e-3f;
+        const f3 q2 = (ld_f3(P.light_center) + f3{0.25f, 0.0f, 0.0f} * ux2) + f3{0.0f, 0.0f, 0.25f} * uy2;
+        f3 L2 = q2 - p2;
+        const float dist2 = length(L2);
+        const float inv2 = 1.0f / fmaxf(dist2, 1e-3f);
+        L2 = L2 * inv2;
+        f3 lc2 = ld_f3(P.light_color) * (inv2 * inv2);
+        lc2 = lc2 * saturate(dot(-L2, f3{0.0f, -1.0f, 0.0f}));
+        lc2 = lc2 * saturate(dot(N2, L2));
+        const f3 c2 = lc2 * (cz(s.thr) * df);
+        cz_sink(c2);
+        cz_sink(f3{fminf(p2.x, q2.x), fminf(p2.y, q2.y), fminf(p2.z, q2.z)});
+        cz_sink(f3{fmaxf(p2.x, q2.x), fmaxf(p2.y, q2.y), fmaxf(p2.z, q2.z)});
+        if (b + 1 < B) {
+            float sp2, cp2;
+            sincos_pt(6.28318548f * cz(ux), &sp2, &cp2);
+            const float ct2 = sqrtf(cz(uy));
+            const float st2 = sqrtf(1.0f - ct2 * ct2);
+            cz_sink((r2 * (st2 * cp2) + N2 * ct2) + f2 * (st2 * sp2));
+        }
+    }
+#endif
     const f3 lcen = ld_f3(P.light_center);
     const f3 q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
     f3 L = q - p;
@@ -189,6 +251,13 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         }
         return true;
     }
+#if RT_CENSUS == 3
+    if (lit) {
+        f3 p2 = cz(p), L2 = cz(L);
+        cz_sink(any_hit<GEO, SPH, b == 0 && !SPH>(sv, p2, L2, 0.0f, cz(dist) - 1e-3f, cz(seg_lo), cz(seg_hi)) ? 1.0f
+                                                                                                            : 0.0f);
+    }
+#endif
     if (lit && !any_hit<GEO, SPH, b == 0 && !SPH>(sv, p, L, 0.0f, dist - 1e-3f, seg_lo, seg_hi))  // :79-85
         s.acc = s.acc + contrib;                           // :87-89
     if (b + 1 < B) {
@@ -211,6 +280,14 @@ __device__ __forceinline__ bool bounce(const KParams& P, const SceneView& sv, Pa
     float t = 1000.0f;                                      // max_distance (sampling.metal:155)
     // Camera rays of an 8x8 tile are coherent: cull with their segment boxes.
     const int id = closest_hit<GEO, SPH, b == 0, (b == 0 ? 0 : 1)>(sv, s.o, s.d, 0.001f, &t);  // min_distance :154
+#if RT_CENSUS == 2
+    {
+        f3 o2 = cz(s.o), d2 = cz(s.d);
+        float t2 = cz(1000.0f);
+        const int id2 = closest_hit<GEO, SPH, b == 0, (b == 0 ? 0 : 1)>(sv, o2, d2, 0.001f, &t2);
+        cz_sink(t2 + (float)id2);
+    }
+#endif
     if (id < 0) return false;                               // :51-53
     return shade<b, B, GEO, SPH, SMALL, false, GEO == kGeoSphLds || (RT_TRI_STASH && GEO == kGeoTriBvh)>(P, sv, s, id,
                                                                                                  t);
@@ -674,6 +751,16 @@ void path_trace_kernel(KParams P) {
             s.d = normalize((cu * sh + cv * th) - cw);
             s.o = ld_f3(P.cam_pos);
             s.thr = f3{1.0f, 1.0f, 1.0f};
+#if RT_CENSUS == 1
+            {
+                const uint32_t i2 = cz(s.i);
+                const float jx2 = halton_dim<0, SMALL>(i2);
+                const float jy2 = halton_dim<1, SMALL, GEO == kGeoPairClu>(i2, sv.htab);
+                const float sx2 = ((cz(fx) + jx2) / fW) * 2.0f - 1.0f;
+                const float ty2 = -(((cz(fy) + jy2) / fH) * 2.0f - 1.0f);
+                cz_sink(normalize((cu * (sx2 * P.halfW) + cv * (ty2 * P.halfH)) - cw));
+            }
+#endif
 #ifndef RT_TIMING_NO_TRACE  // timing-only A/B (tools/ab_kernel.sh): camera, Halton jitter and sums alone
             trace_path<B, GEO, SPH, SMALL>(P, sv, s);                       // :47-102
 #else
@@ -693,6 +780,13 @@ void path_trace_kernel(KParams P) {
             // sample order, no LDS-pipe traffic.  Only the leaders' sums are kept.
             const uint32_t t2 = opaque_tid(), sub2 = t2 % L, slot = t2 / L;
             f3 acc{lum_s[3 * slot], lum_s[3 * slot + 1], lum_s[3 * slot + 2]};
+#if RT_CENSUS == 6
+            {
+                f3 a2 = cz(acc);
+                row_sum_in_order<L, 0>::run(a2, cz(s.acc), r * L, P.spp);
+                cz_sink(a2);
+            }
+#endif
             row_sum_in_order<L, 0>::run(acc, s.acc, r * L, P.spp);  // :103
             if (sub2 == 0) {
                 lum_s[3 * slot] = acc.x;
