@@ -556,10 +556,18 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
     K.row_start = start;
     K.row_step = step;
     K.row_count = count;
-    if (const size_t pb = rt::mis_part_bytes(K.camera_rays, pixels)) {
-        if ((st = ensure_staging(c, &c->d_mis_part, &c->mis_part_cap, pb, "hipMalloc(mis rays)")) != RT_OK)
+    const size_t pb = rt::mis_part_bytes(K.camera_rays, pixels);
+    if (c->mis_part_cap > 2 * pb) {  // a much smaller (or unsplit) frame: give the memory back
+        const hipError_t e0 = hipStreamSynchronize(c->stream);  // the last launch may still read it
+        if (e0 != hipSuccess) return hip_fail(c, RT_ERR_LAUNCH, "hipStreamSynchronize(mis)", e0);
+        (void)hipFree(c->d_mis_part);
+        c->d_mis_part = nullptr;
+        c->mis_part_cap = 0;
+    }
+    if (pb) {
+        if ((st = ensure_staging(c, &c->d_mis_part, &c->mis_part_cap, pb, "hipMalloc(mis records)")) != RT_OK)
             return st;
-        K.part = reinterpret_cast<float4*>(c->d_mis_part);
+        K.part = reinterpret_cast<float*>(c->d_mis_part);
     }
 
     hipError_t e;

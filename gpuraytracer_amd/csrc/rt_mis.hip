@@ -545,13 +545,34 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
                 }
             }
         }
-        if (SPLIT) {  // this ray's result; the pixel's sum is mis_sum_kernel's
-            if (i < P.camera_rays) {
-                uint32_t x, j;
-                pixel_of(opaque_u32(threadIdx.x), x, j);
-                const size_t npix = (size_t)P.row_count * (size_t)P.W;
-                P.part[(size_t)i * npix + (size_t)j * (size_t)P.W + x] =
-                    make_float4(c.x, c.y, c.z, has ? 1.0f : 0.0f);
+        if (SPLIT) {  // mis_sum_kernel adds the records in ray order
+            const uint32_t t3 = opaque_u32(threadIdx.x);
+            uint32_t x, j;
+            pixel_of(t3, x, j);
+            const size_t npix = (size_t)P.row_count * (size_t)P.W, px = (size_t)j * (size_t)P.W + x;
+            if (r == 0) {
+                // record 0: round 0's rays summed in ray order from +0 -- the
+                // first ML additions of the pixel's sum (:652-677)
+                const int base = (int)((t3 & 63u) - (t3 & 63u) % ML);
+                f3 acc{0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (uint32_t k = 0; k < ML; ++k) {
+                    const f3 ck{__shfl(c.x, base + (int)k), __shfl(c.y, base + (int)k), __shfl(c.z, base + (int)k)};
+                    if (__shfl((int)has, base + (int)k) != 0) acc = acc + ck;
+                }
+                if ((t3 & 63u) % ML == 0) {
+                    P.part[px] = acc.x;
+                    P.part[npix + px] = acc.y;
+                    P.part[2 * npix + px] = acc.z;
+                }
+            } else if (i < P.camera_rays) {
+                // record i - ML + 1: this ray's c, which is +0 without a hit --
+                // adding it equals skipping it (the sum starts at +0, so it is
+                // never -0, and x + (+0) == x for every other x, NaN included)
+                float* rec = P.part + (size_t)3 * (i - ML + 1u) * npix + px;
+                rec[0] = c.x;
+                rec[npix] = c.y;
+                rec[2 * npix] = c.z;
             }
             continue;
         }
@@ -590,24 +611,28 @@ __global__ void mis_sum_kernel(MisParams P) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
     if (x >= (uint32_t)P.W) return;
     const size_t npix = (size_t)P.row_count * (size_t)P.W, o = (size_t)j * (size_t)P.W + x;
-    f3 acc{0.0f, 0.0f, 0.0f};
-    for (uint32_t i = 0; i < P.camera_rays; ++i) {
-        const float4 v = P.part[(size_t)i * npix + o];
-        if (v.w != 0.0f) acc = acc + f3{v.x, v.y, v.z};
+    f3 acc{P.part[o], P.part[npix + o], P.part[2 * npix + o]};  // rays 0 .. ML-1
+    for (uint32_t i = kMisLanes; i < P.camera_rays; ++i) {
+        const float* rec = P.part + (size_t)3 * (i - kMisLanes + 1u) * npix + o;
+        acc = acc + f3{rec[0], rec[npix], rec[2 * npix]};
     }
     mis_store(P, o, acc);
 }
 
 constexpr size_t kMisStashBytes = 15u * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc, strategy sum
 
-// SPLIT launches (RT_MIS_SPLIT): the per-ray results buffer, 16 B per camera ray
-// and pixel; 0 (no split) when it would exceed kMisPartMax or the split is off.
+// SPLIT launches (RT_MIS_SPLIT): the records buffer, 12 B per record and pixel
+// (3 float planes per record): record 0 = round 0's rays already summed, then
+// one record per later ray -- camera_rays - ML + 1 records (round 5: 16 B per
+// ray with a hit flag, 46 MB at 800x600 x 6 rays; now 28.8 MB); 0 (no split)
+// when it would exceed kMisPartMax or the split is off.
 #ifndef RT_MIS_SPLIT
 #define RT_MIS_SPLIT 1
 #endif
-constexpr size_t kMisPartMax = (size_t)1 << 30;
+constexpr size_t kMisPartMax = (size_t)256 << 20;
 size_t mis_part_bytes(uint32_t camera_rays, size_t pixels) {
-    const size_t b = (size_t)camera_rays * pixels * sizeof(float4);
+    if (camera_rays <= kMisLanes) return 0u;
+    const size_t b = (size_t)(camera_rays - kMisLanes + 1u) * pixels * 3u * sizeof(float);
     return (RT_MIS_SPLIT && camera_rays > kMisLanes && b <= kMisPartMax) ? b : 0u;
 }
 

@@ -353,6 +353,57 @@ __device__ __forceinline__ bool lds_node_hit_nf(const uint4& e, const RayBox& rb
 #define RT_SPH_PARK_DEN 2
 #endif
 constexpr int kSphParkDen = RT_SPH_PARK_DEN;
+// RT_SPH_SEL: every lane runs both halves of a step (box test and
+// discriminant) and keeps its entry's by selects; RT_SPH_CHK: steps between
+// two checks of the parking condition (a lane that parks in between holds
+// still).  Round 6, config 4 (Msamples/s): every step 3,512-3,520; selects
+// 3,059 (selects + every 2 / 3 steps 3,112 / 3,127); branch-form steps checked
+// every 2 / 3 / 4 / 5 / 6 / 8 / 12 steps 3,738 / 3,811 / 3,832 / 3,845 / 3,868 /
+// 3,829 / 3,791, every 6 or 8 with the roots at 1/3 3,885 / 3,893
+// (profiles/r6/ab_results.md)
+#ifndef RT_SPH_SEL
+#define RT_SPH_SEL 0
+#endif
+#ifndef RT_SPH_CHK
+#define RT_SPH_CHK 6
+#endif
+// One step of a lane's compact sphere-BVH walk in select form (RT_SPH_SEL).
+__device__ __forceinline__ void sphere_step_sel(const uint4* __restrict__ ent, uint32_t& idx, uint32_t& leaf,
+                                                float& pb, float& pdisc, const RayBox& rb, f3 o, f3 d,
+                                                float a, float tmin, float best) {
+    const uint4 e = ent[idx];
+    const bool inner = (e.w & 0x80000000u) != 0u;
+    const bool h = lds_node_hit_nf(e, rb, tmin, best);
+    const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y), __uint_as_float(e.z)};
+    const float bq = 2.0f * dot(oc, d);
+    const float cc = dot(oc, oc) - __uint_as_float(e.w);
+    const float disc = bq * bq - (4.0f * a) * cc;
+    const bool park = !inner && disc > 0.0f;  // sph_test up to the discriminant (shaders_old.metal:108-136)
+    leaf = park ? idx : leaf;
+    pb = park ? bq : pb;
+    pdisc = park ? disc : pdisc;
+    idx = (inner && !h) ? (e.w & 0x7FFFFFFFu) : idx + 1;
+}
+// The same step with the kernel's branches (the shipped form).
+__device__ __forceinline__ void sphere_step_br(const uint4* __restrict__ ent, uint32_t& idx, uint32_t& leaf,
+                                               float& pb, float& pdisc, const RayBox& rb, f3 o, f3 d,
+                                               float a, float tmin, float best) {
+    const uint4 e = ent[idx];
+    if (e.w & 0x80000000u) {
+        idx = lds_node_hit_nf(e, rb, tmin, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
+    } else {  // sph_test up to the discriminant (shaders_old.metal:108-136)
+        const f3 oc = o - f3{__uint_as_float(e.x), __uint_as_float(e.y), __uint_as_float(e.z)};
+        const float bq = 2.0f * dot(oc, d);
+        const float cc = dot(oc, oc) - __uint_as_float(e.w);
+        const float disc = bq * bq - (4.0f * a) * cc;
+        if (disc > 0.0f) {
+            leaf = idx;
+            pb = bq;
+            pdisc = disc;
+        }
+        idx = idx + 1;  // a leaf's escape is the next entry
+    }
+}
 template <bool ANY>
 __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const uint16_t* __restrict__ ids,
                                             uint32_t nN, uint32_t nT, f3 o, f3 d, float tmin, float& best,
@@ -375,7 +426,12 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
             if (__builtin_amdgcn_ballot_w64(adv) == 0) break;
             RT_STAT(ST + 2, 1);
             RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(adv)));
+#if RT_SPH_SEL
+            if (adv) sphere_step_sel(ent, idx, leaf, pb, pdisc, rb, o, d, a, tmin, best);
+            if (false) {
+#else
             if (adv) {
+#endif
                 const uint4 e = ent[idx];
                 if (e.w & 0x80000000u) {
                     idx = lds_node_hit_nf(e, rb, tmin, best) ? idx + 1 : (e.w & 0x7FFFFFFFu);
@@ -393,6 +449,19 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
                     idx = idx + 1;  // a leaf's escape is the next entry
                 }
             }
+#if RT_SPH_CHK > 1
+#pragma unroll
+            for (int q = 1; q < RT_SPH_CHK; ++q) {  // more steps before the next check
+                RT_STAT(ST + 2, 1);
+                RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(idx < end && leaf == kNone)));
+                if (idx < end && leaf == kNone) {
+                    if (RT_SPH_SEL)
+                        sphere_step_sel(ent, idx, leaf, pb, pdisc, rb, o, d, a, tmin, best);
+                    else
+                        sphere_step_br(ent, idx, leaf, pb, pdisc, rb, o, d, a, tmin, best);
+                }
+            }
+#endif
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
             if (kSphParkDen * parked >= live) break;
@@ -520,15 +589,29 @@ __device__ __forceinline__ bool tri_cbvh_any_packet(const uint4* __restrict__ cn
 // entries are visited in the same order and ranked by (t, id): the same result.
 // the parked leaves are tested once they are >= 1/kTriParkDen of the live lanes
 // (100k triangles: 1/4 738, 1/2 701, 3/4 570, 1/8 707 Msamples/s; round 5 with
-// near/far boxes: 1/3 894-896, 1/4 887-890, 1/2 872, 1/6 865, 1/8 843)
+// near/far boxes: 1/3 894-896, 1/4 887-890, 1/2 872, 1/6 865, 1/8 843; round 6
+// with select-form steps checked every 4: 1/4 1,115, 1/3 1,111, 1/2 1,078)
 #ifndef RT_TRI_PARK_DEN
-#define RT_TRI_PARK_DEN 3
+#define RT_TRI_PARK_DEN 4
 #endif
 constexpr int kTriParkDen = RT_TRI_PARK_DEN;
 // RT_TRI_LOOKAHEAD: the next sequential entry requested one step early
 // (100k triangles 888 -> 787 Msamples/s: 4 more VGPRs, 20 spilled; off)
 #ifndef RT_TRI_LOOKAHEAD
 #define RT_TRI_LOOKAHEAD 0
+#endif
+// RT_TRI_SEL: the step's outcome by selects (no exec-mask branches around the
+// box test); RT_TRI_CHK: steps between two checks of the parking condition
+// (the two ballots, popcounts and compares of the check are a third of a
+// step's instructions; a lane that parks in between holds still).  Round 6,
+// 100k triangles (Msamples/s): branch form, check every step 988-990;
+// selects 1,029; check every 2 steps 1,068; both: every 2 / 3 / 4 / 6 / 8
+// steps 1,082-1,093 / 1,103 / 1,111 / 1,109 / 1,086 (profiles/r6/ab_results.md)
+#ifndef RT_TRI_SEL
+#define RT_TRI_SEL 1
+#endif
+#ifndef RT_TRI_CHK
+#define RT_TRI_CHK 4
 #endif
 template <bool ANY>
 __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, const float4* __restrict__ tri,
@@ -575,6 +658,12 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
                     cur = cn[idx < last ? idx : last];
                 }
                 seq = cn[idx + 1u < last ? idx + 1u : last];
+#elif RT_TRI_SEL
+                const uint4 e = cn[idx];
+                const bool inner = (e.w & 0x80000000u) != 0u;
+                const bool h = lds_node_hit_nf(e, rb, tmin, best);
+                leaf = (h && !inner) ? e.w : leaf;
+                idx = (h || !inner) ? idx + 1 : (e.w & 0x7FFFFFFFu);
 #else
                 const uint4 e = cn[idx];
                 const bool inner = (e.w & 0x80000000u) != 0u;
@@ -590,6 +679,21 @@ __device__ __forceinline__ void tri_cbvh_walk(const uint4* __restrict__ cn, cons
                 }
 #endif
             }
+#if RT_TRI_CHK > 1
+            // more steps before the next check (a parked lane holds still)
+#pragma unroll
+            for (int q = 1; q < RT_TRI_CHK; ++q) {
+                RT_STAT(ST + 2, 1);
+                RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(idx < end && leaf == kNone)));
+                if (idx < end && leaf == kNone) {
+                    const uint4 e = cn[idx];
+                    const bool inner = (e.w & 0x80000000u) != 0u;
+                    const bool h = lds_node_hit_nf(e, rb, tmin, best);
+                    leaf = (h && !inner) ? e.w : leaf;
+                    idx = (h || !inner) ? idx + 1 : (e.w & 0x7FFFFFFFu);
+                }
+            }
+#endif
             const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
             const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
             if (kTriParkDen * parked >= live) break;
@@ -727,6 +831,9 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
     return mask;
 }
 
+#ifndef RT_PAIR_SEL
+#define RT_PAIR_SEL 0
+#endif
 // Exact pair test (the same arithmetic as the brute-force loops) with the
 // hit ranked lexicographically by (t, triangle id): pairs are visited out of
 // id order here, and (t, id) order is what the id-ordered scan with strict
@@ -738,6 +845,18 @@ __device__ __forceinline__ void pair_test_rank(const float4* r, uint32_t k, f3 o
     const PairDots q = pair_dots(r0, r1, r2, r3, r4, o, d);
     const bool pa = bary_ok(q.denA, q.a1, q.a2);
     const bool pb = bary_ok(q.denB, q.b1, q.b2);
+#if RT_PAIR_SEL  // A/B: the first division by every lane, kept by selects (no exec branch)
+    {
+        const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
+        const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
+        const int ia = (int)(pa ? 2 * k : 2 * k + 1);
+        const bool take = (pa || pb) && t > tmin && (t < *best || (!ANY && t == *best && ia < *id));
+        if (!ANY) *best = take ? t : *best;
+        *id = take ? ia : *id;
+    }
+    if (pa && pb) {
+        {
+#else
     if (pa || pb) {
         const f3 nsel = pa ? f3{r2.y, r2.z, r2.w} : f3{r3.w, r4.x, r4.y};
         const float t = pair_t(nsel, q.tv, pa ? q.denA : q.denB);
@@ -747,6 +866,7 @@ __device__ __forceinline__ void pair_test_rank(const float4* r, uint32_t k, f3 o
             *id = ia;
         }
         if (pa && pb) {
+#endif
             const float t2 = pair_t(f3{r3.w, r4.x, r4.y}, q.tv, q.denB);
             const int ib = (int)(2 * k + 1);
             if (t2 > tmin && (t2 < *best || (!ANY && t2 == *best && ib < *id))) {
