@@ -38,6 +38,7 @@ struct rt_ctx {
     float4* d_clusters = nullptr;
     uint32_t* d_sph_lds = nullptr;
     uint16_t* d_sph_lds_id = nullptr;
+    uint4* d_sph_box = nullptr;      // the leaf-box layout of the sphere BVH (rt_scene.hpp sph_box)
     float4* d_sph_isect = nullptr;
     float4* d_sph_shade = nullptr;
     float4* d_sph_nodes = nullptr;
@@ -137,6 +138,7 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_clusters);
     (void)hipFree(c->d_sph_lds);
     (void)hipFree(c->d_sph_lds_id);
+    (void)hipFree(c->d_sph_box);
     (void)hipFree(c->d_sph_isect);
     (void)hipFree(c->d_sph_shade);
     (void)hipFree(c->d_sph_nodes);
@@ -242,6 +244,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.sph_isect = c->d_sph_isect;
     K.sph_lds = c->scene.sph_lds.empty() ? nullptr : c->d_sph_lds;
     K.sph_lds_id = c->d_sph_lds_id;
+    K.sph_box = c->scene.sph_box.empty() ? nullptr : c->d_sph_box;
     K.sph_shade = c->d_sph_shade;
     K.sph_nodes = c->d_sph_nodes;
     K.sph_perm = c->d_sph_perm;
@@ -724,6 +727,7 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
             (e = upload(&c->d_clusters, s.clusters.data(), s.clusters.size() * sizeof(float), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_lds, s.sph_lds.data(), s.sph_lds.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_lds_id, s.sph_lds_id.data(), s.sph_lds_id.size() * sizeof(uint16_t), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_sph_box, s.sph_box.data(), s.sph_box.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_isect, s.sph_isect.data(), s.sph_isect.size() * sizeof(rt::SphIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_shade, s.sph_shade.data(), s.sph_shade.size() * sizeof(rt::SphShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_nodes, s.sph_nodes.data(), s.sph_nodes.size() * sizeof(rt::BvhNode), c->stream)) != hipSuccess ||

@@ -620,6 +620,8 @@ void path_trace_kernel(KParams P) {
         if (GEO == kGeoSphLds) {  // the compact sphere BVH (8 layouts) stays in global memory (L2)
             sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
             sv.sid = P.sph_lds_id;
+            sv.sbox = P.sph_box;
+            sv.nSB = P.nN;
             __shared__ float sph_stash[GEO == kGeoSphLds ? 6 * kSphBlockThreads : 1];
             sv.xstash = sph_stash;
         }
@@ -864,6 +866,8 @@ void path_trace_sorted_kernel(
     sv.nN = SPH ? (GEO == kGeoSphLds ? P.nE : P.nN) : 0u;
     sv.sent = reinterpret_cast<const uint4*>(P.sph_lds);
     sv.sid = P.sph_lds_id;
+    sv.sbox = P.sph_box;
+    sv.nSB = P.nN;
     sv.tnode = P.tri_nodes;
     sv.tsorted = P.tri_sorted;
     sv.tperm = P.tri_perm;

@@ -47,6 +47,7 @@ struct KParams {
     const float4* sph_shade;  // 3 float4 per sphere, by id (SphShade)
     const uint32_t* sph_lds;  // compact sphere BVH (8 layouts x nE x 16 B), or null
     const uint16_t* sph_lds_id;  // sphere id per compact entry
+    const uint4* sph_box;     // the same BVH with leaf boxes: 8 layouts x nN entries, or null
     const uint4* tri_nodes;   // triangle BVH: 8 compact layouts x nTN nodes, or null
     const float4* tri_sorted; // 3 float4 per triangle, BVH leaf order
     const uint32_t* tri_perm; // BVH leaf order -> triangle id

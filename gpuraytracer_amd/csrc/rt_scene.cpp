@@ -414,6 +414,43 @@ static uint16_t half_dir(float x, int dir) {
     return b;
 }
 
+// The leaf-box layout (CompiledScene::sph_box): one entry per node of every
+// octant layout, escapes = node indices over all layouts.
+static void build_sphere_box(CompiledScene* out) {
+    out->sph_box.clear();
+    const uint32_t nn = out->sph_layout_nodes;
+    if (nn == 0 || out->sph_isect.size() >= (1u << 24)) return;
+    std::vector<uint32_t> ent;
+    ent.reserve((size_t)8 * nn * 4);
+    for (int oct = 0; oct < 8; ++oct) {
+        const BvhNode* L = out->sph_nodes.data() + (size_t)oct * nn;
+        const uint32_t lay_base = (uint32_t)oct * nn;
+        for (uint32_t i = 0; i < nn; ++i) {
+            const BvhNode& n = L[i];
+            uint16_t h[6];
+            for (int a = 0; a < 3; ++a) {
+                if (!isfinite(n.lo[a]) || !isfinite(n.hi[a])) return;
+                h[a] = half_dir(n.lo[a], -1);
+                h[3 + a] = half_dir(n.hi[a], +1);
+                if ((oct >> a) & 1) std::swap(h[a], h[3 + a]);  // near/far, as build_sphere_lds
+            }
+            uint32_t w;
+            if (n.leaf == 0) {
+                if (n.escape > nn) return;
+                w = (lay_base + n.escape) | 0x80000000u;
+            } else {
+                const uint32_t first = n.leaf & 0xFFFFFFu, cnt = n.leaf >> 24;
+                if (cnt == 0 || cnt > 128 || n.escape != i + 1) return;
+                w = first | (cnt - 1u) << 24;
+            }
+            const uint32_t q[4] = {h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,
+                                   h[4] | (uint32_t)h[5] << 16, w};
+            ent.insert(ent.end(), q, q + 4);
+        }
+    }
+    out->sph_box.swap(ent);
+}
+
 static void build_sphere_lds(CompiledScene* out) {
     out->sph_lds.clear();
     out->sph_lds_id.clear();
@@ -492,6 +529,7 @@ static void build_sphere_lds(CompiledScene* out) {
 static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint32_t n,
                              float margin, const BuildOptions& opt) {
     out->sph_isect.clear();
+    out->sph_box.clear();
     out->sph_perm.clear();
     out->sph_nodes.clear();
     out->sph_layout_nodes = 0;
@@ -521,6 +559,7 @@ static void build_sphere_bvh(CompiledScene* out, const SphereGPU* spheres, uint3
         memcpy(out->sph_isect[k].q, q, sizeof(q));
     }
     build_sphere_lds(out);
+    build_sphere_box(out);
 }
 
 // Triangle BVH built on the host with binned SAH:

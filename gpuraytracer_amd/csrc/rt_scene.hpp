@@ -105,6 +105,11 @@ struct CompiledScene {
     // its sphere id in sph_lds_id.  Empty when the tree does not qualify.
     std::vector<uint32_t> sph_lds;      // 8 layouts x sph_lds_entries x 4 words
     std::vector<uint16_t> sph_lds_id;   // 8 layouts x sph_lds_entries
+    // The same tree with LEAF BOXES (round 6): one 16-B entry per node in the
+    // same near/far fp16 form, inner nodes as above, a leaf node = its padded
+    // box + (first leaf-order sphere | (count - 1) << 24); the spheres stay in
+    // sph_isect (leaf order).  Every step of a walk is then the same box test.
+    std::vector<uint32_t> sph_box;      // 8 layouts x sph_layout_nodes x 4 words
     // Box clusters over the pair records: 28 floats each,
     // (u0.xyz, lo0) (u1.xyz, lo1) (u2.xyz, lo2) (hi0, hi1, hi2, flags)
     // (m0, m1, m2, m3) (m4, m5, all, 0) (w0, w1, w2, 0): an oriented box (padded

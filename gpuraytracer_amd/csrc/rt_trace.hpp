@@ -160,6 +160,8 @@ struct SceneView {
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
     const uint4* sent;        // compact sphere BVH entries (kGeoSphLds): 8 octant layouts, global
     const uint16_t* sid;      // sphere id of each compact entry (leaves), global
+    const uint4* sbox;        // the sphere BVH with leaf boxes (RT_SPH_LEAFBOX): 8 layouts of nSB entries
+    uint32_t nSB;
     const float4* shade;      // MIS shading records, 3 float4 per triangle (rt_mis.hip)
     float* xstash;            // MIS: per-lane primary hit (p, din), SoA in LDS (rt_mis.hip)
 };
@@ -484,6 +486,89 @@ __device__ __forceinline__ void sphere_walk(const uint4* __restrict__ ent, const
                 if (t < best || s < id) {
                     best = t;
                     id = s;
+                }
+            }
+            leaf = kNone;
+        }
+    }
+}
+
+// Per-lane walk of the sphere BVH with LEAF BOXES (rt_scene.cpp
+// build_sphere_box; RT_SPH_LEAFBOX): every entry is a near/far fp16 box -- a
+// leaf's box is its padded sphere box, like any node's -- so every step of
+// every lane is the same select-form box test (the compact walk above runs
+// the box test and the discriminant side by side whenever a wave holds lanes
+// at both kinds of entry, ~33 VALU a step).  A lane whose leaf box is hit
+// parks the leaf; the parked lanes' spheres are tested with sph_test (the
+// discriminant, then the IEEE roots) once they are >= 1/kSphBoxParkDen of the
+// walkers, checked every kSphBoxChk steps.  Candidates are ranked by
+// (t, sphere id) as in every walk: the brute-force answer.
+// Config 4 (Msamples/s, profiles/r6/ab_results.md): the compact walk checked
+// every step 3,512-3,520, every 6 steps 3,867-3,874; leaf boxes checked every
+// 2 / 4 / 5 / 6 / 8 steps 3,883 / 4,018 / 4,027 / 4,042-4,044 / 4,037 with the
+// roots at 1/3 (1/2 and 1/4 at every 6: 3,989 / 4,038); leaves of 2 / 3 / 4
+// spheres 3,883 / 3,734 / 3,591
+#ifndef RT_SPH_LEAFBOX
+#define RT_SPH_LEAFBOX 1
+#endif
+#ifndef RT_SPH_BOX_PARK_DEN
+#define RT_SPH_BOX_PARK_DEN 3
+#endif
+#ifndef RT_SPH_BOX_CHK
+#define RT_SPH_BOX_CHK 6
+#endif
+template <bool ANY>
+__device__ __forceinline__ void sphere_walk_box(const uint4* __restrict__ ent, const float4* __restrict__ sph,
+                                                const uint32_t* __restrict__ perm, uint32_t nN, uint32_t nT, f3 o,
+                                                f3 d, float tmin, float& best, int& id) {
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    const float a = dot(d, d);
+    const RayBox rb = ray_box(o, d);
+    uint32_t idx = octant(d) * nN;
+    const uint32_t end = idx + nN;
+    if (ANY && id >= 0) idx = end;
+    uint32_t leaf = kNone;
+    [[maybe_unused]] constexpr int ST = ANY ? 24 : 16;
+    RT_STAT(ST, 1);
+    RT_STAT(ST + 1, __popcll(__ballot(1)));
+    for (;;) {
+        for (;;) {
+            if (__builtin_amdgcn_ballot_w64(idx < end && leaf == kNone) == 0) break;
+#pragma unroll
+            for (int q = 0; q < RT_SPH_BOX_CHK; ++q) {
+                RT_STAT(ST + 2, 1);
+                RT_STAT(ST + 3, __popcll(__builtin_amdgcn_ballot_w64(idx < end && leaf == kNone)));
+                if (idx < end && leaf == kNone) {
+                    const uint4 e = ent[idx];
+                    const bool inner = (e.w & 0x80000000u) != 0u;
+                    const bool h = lds_node_hit_nf(e, rb, tmin, best);
+                    leaf = (h && !inner) ? e.w : leaf;
+                    idx = (h || !inner) ? idx + 1 : (e.w & 0x7FFFFFFFu);
+                }
+            }
+            const int parked = __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone));
+            const int live = __popcll(__builtin_amdgcn_ballot_w64(idx < end || leaf != kNone));
+            if (RT_SPH_BOX_PARK_DEN * parked >= live) break;
+        }
+        if (__builtin_amdgcn_ballot_w64(leaf != kNone) == 0) break;
+        RT_STAT(ST + 5, 1);
+        RT_STAT(ST + 6, __popcll(__builtin_amdgcn_ballot_w64(leaf != kNone)));
+        if (leaf != kNone) {  // the parked leaf's spheres (shaders_old.metal:108-136)
+            const uint32_t first = leaf & 0xFFFFFFu, cnt = (leaf >> 24) + 1u;
+            for (uint32_t k = first; k < first + cnt; ++k) {
+                float t;
+                if (ANY) {
+                    if (sph_test(sph[k], o, d, a, tmin, best, &t)) {
+                        id = 0;
+                        idx = end;
+                        break;
+                    }
+                } else if (sph_test(sph[k], o, d, a, tmin, 3.0e38f, &t) && t <= best) {
+                    const int s = (int)(nT + perm[k]);
+                    if (t < best || s < id) {
+                        best = t;
+                        id = s;
+                    }
                 }
             }
             leaf = kNone;
@@ -1067,7 +1152,9 @@ __device__ __forceinline__ int closest_hit(const SceneView& sv, f3& o, f3& d, fl
             }
         }
     }
-    if (SPH && GEO == kGeoSphLds)
+    if (SPH && GEO == kGeoSphLds && RT_SPH_LEAFBOX)
+        sphere_walk_box<false>(sv.sbox, sv.sph, sv.sph_perm, sv.nSB, sv.nT, o, d, tmin, best, id);
+    else if (SPH && GEO == kGeoSphLds)
         sphere_walk<false>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, best, id);
     else if (SPH)
         sphere_closest(sv.node, sv.sph, sv.sph_perm, sv.nN, sv.nT, o, d, tmin, best, id);
@@ -1135,7 +1222,10 @@ __device__ __forceinline__ bool any_hit(const SceneView& sv, f3& o, f3& d, float
     if (SPH && GEO == kGeoSphLds) {
         float tm = tmax;
         int id = -1;
-        sphere_walk<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id);
+        if (RT_SPH_LEAFBOX)
+            sphere_walk_box<true>(sv.sbox, sv.sph, sv.sph_perm, sv.nSB, sv.nT, o, d, tmin, tm, id);
+        else
+            sphere_walk<true>(sv.sent, sv.sid, sv.nN, sv.nT, o, d, tmin, tm, id);
         return id >= 0;
     }
     if (SPH) return sphere_any(sv.node, sv.sph, sv.nN, o, d, tmin, tmax);
