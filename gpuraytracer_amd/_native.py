@@ -155,6 +155,7 @@ SIGNATURES = {
     "rt_destroy": (ctypes.c_int, [_P]),
     "rt_last_launch": (ctypes.c_int, [_P, ctypes.POINTER(LaunchInfo)]),
     "rt_build_info": (ctypes.c_int, [_P, ctypes.POINTER(BuildStats)]),
+    "rt_math_selfcheck": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "rt_comm_unique_id": (ctypes.c_int, [_P]),
     "rt_comm_init": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P]),
     "rt_render_gather": (ctypes.c_int, [_P, ctypes.POINTER(RenderParamsC), _P, _P]),

@@ -951,6 +951,18 @@ int rt_place_tiles_host(const void* gathered, int32_t width, int32_t height, int
     return RT_OK;
 }
 
+int rt_math_selfcheck(uint64_t* mismatches) {
+    if (!mismatches) return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(nullptr, RT_ERR_NO_DEVICE, "no HIP device");
+    unsigned long long bad[2] = {0, 0};
+    const hipError_t e = rt::math_selfcheck(bad);
+    if (e != hipSuccess) return hip_fail(nullptr, RT_ERR_LAUNCH, "math_selfcheck", e);
+    mismatches[0] = bad[0];
+    mismatches[1] = bad[1];
+    return RT_OK;
+}
+
 int rt_build_info(const rt_ctx* c, rt_build_stats* info) {
     if (!c || !info) return fail(nullptr, RT_ERR_INVALID_ARG, "null argument");
     memset(info, 0, sizeof(*info));

@@ -176,7 +176,7 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     const f3 q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
     f3 L = q - p;
     const float dist = length(L);
-    const float inv = 1.0f / fmaxf(dist, 1e-3f);
+    const float inv = rcp_cr(fmaxf(dist, 1e-3f));
     L = L * inv;
     f3 lc = ld_f3(P.light_color) * (inv * inv);
     lc = lc * saturate(dot(-L, f3{0.0f, -1.0f, 0.0f}));
@@ -194,8 +194,8 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         const float cv = halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
         float sp, cp;
         sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
-        const float ct = sqrtf(cv);
-        const float st = sqrtf(1.0f - ct * ct);
+        const float ct = sqrt_cr(cv);
+        const float st = sqrt_cr(1.0f - ct * ct);
         d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
     }
     if (FUSE && b + 1 < B) {
@@ -924,6 +924,23 @@ void path_trace_sorted_kernel(
     }
 }
 
+// rt_math_selfcheck: the shipped sqrt_cr / rcp_cr (rt_math.h) against the
+// IEEE sqrtf / division on every float bit pattern b in [lo, lo + n): bad[0]
+// counts sqrt mismatches (NaN results compare as NaN), bad[1] reciprocal ones.
+__global__ void math_check_kernel(uint32_t lo, uint32_t n, unsigned long long* bad) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float x = __uint_as_float(lo + i);
+        float y = x;
+        asm volatile("" : "+v"(y));  // an opaque copy: the references stay the IEEE expansions
+        const float s = sqrt_cr(x), sr = sqrtf(y);
+        const float r = rcp_cr(x), rr = 1.0f / y;
+        const bool sbad = !(__float_as_uint(s) == __float_as_uint(sr) || (s != s && sr != sr));
+        const bool rbad = !(__float_as_uint(r) == __float_as_uint(rr) || (r != r && rr != rr));
+        if (sbad) atomicAdd(&bad[0], 1ull);
+        if (rbad) atomicAdd(&bad[1], 1ull);
+    }
+}
+
 __global__ void fill_seeds_kernel(uint32_t* seeds, uint64_t key, uint64_t n) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
          p += (uint64_t)gridDim.x * blockDim.x) {
@@ -1274,6 +1291,21 @@ hipError_t read_debug_stats(unsigned long long* out, int n) {
     (void)n;
     return hipErrorNotSupported;
 #endif
+}
+
+hipError_t math_selfcheck(unsigned long long bad[2]) {
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc((void**)&d, 2 * sizeof(unsigned long long));
+    if (e != hipSuccess) return e;
+    if ((e = hipMemset(d, 0, 2 * sizeof(unsigned long long))) == hipSuccess) {
+        // every float: 2^32 bit patterns in two halves of 2^31
+        hipLaunchKernelGGL(math_check_kernel, dim3(16384), dim3(256), 0, 0, 0u, 0x80000000u, d);
+        hipLaunchKernelGGL(math_check_kernel, dim3(16384), dim3(256), 0, 0, 0x80000000u, 0x80000000u, d);
+        if ((e = hipGetLastError()) == hipSuccess && (e = hipDeviceSynchronize()) == hipSuccess)
+            e = hipMemcpy(bad, d, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d);
+    return e;
 }
 
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream) {

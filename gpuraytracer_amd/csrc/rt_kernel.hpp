@@ -183,6 +183,9 @@ hipError_t build_tri_gsah(const float4* d_tri, uint32_t n, float margin, uint32_
 hipError_t scan_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tile_sums, hipStream_t s);
 
 hipError_t launch_fill_seeds(uint32_t* seeds, uint64_t key, uint64_t n, hipStream_t stream);
+// The shipped short sqrt / reciprocal (rt_math.h sqrt_cr, rcp_cr) against IEEE
+// sqrtf and 1/x over every float on the current device: mismatch counts.
+hipError_t math_selfcheck(unsigned long long bad[2]);
 
 // Rank 0's placement after the gather (rt_place_tiles): frame row y comes from
 // tile y mod N, tile row y / N; `gathered` holds N tiles of tile_bytes back to

@@ -39,9 +39,52 @@ RT_HD f3 cross(f3 a, f3 b) {
     return f3{fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)),
               fmaf(a.x, b.y, -(a.y * b.x))};
 }
-RT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
+// Correctly rounded sqrt and reciprocal in fewer instructions
+// on the device.  For an argument whose magnitude lies in [2^-100, 2^100) the
+// short sequences below equal IEEE sqrtf(x) and 1.0f / x bit for bit -- checked
+// on gfx950 for every float of that range (tools/math_probe.hip; the library's
+// own rt_math_selfcheck runs the shipped functions over every float, tested in
+// tests/test_gpu_parity.py): a hardware rsq + a Goldschmidt/Markstein
+// refinement (7 VALU instead of the compiler's 15-instruction IEEE sqrt), and a
+// hardware rcp + one fma Newton step (3 instead of ~11 with the div_scale /
+// div_fmas / div_fixup sequence).  A wave with any lane outside the range
+// (or a negative sqrt argument) takes the IEEE expansions; +-0 keeps its sign
+// under sqrt.  The host (and the oracle) use sqrtf and division: the same values.
+#ifndef RT_CR_FAST  // 0: the IEEE expansions everywhere (A/B)
+#define RT_CR_FAST 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && RT_CR_FAST
+__device__ __forceinline__ bool rt_cr_domain(uint32_t b) {  // magnitude bits in [2^-100, 2^100)
+    return b - 0x0D800000u < 0x71800000u - 0x0D800000u;
+}
+__device__ __forceinline__ float sqrt_cr(float x) {
+    const bool ok = x == 0.0f || rt_cr_domain(__float_as_uint(x));  // positive x only (sign bit set fails)
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+        const float r = __builtin_amdgcn_rsqf(x);
+        float s = x * r, h = 0.5f * r;
+        const float e = fmaf(-s, h, 0.5f);
+        s = fmaf(s, e, s);
+        h = fmaf(h, e, h);
+        const float d = fmaf(-s, s, x);
+        const float v = fmaf(d, h, s);
+        return x == 0.0f ? x : v;
+    }
+    return sqrtf(x);
+}
+__device__ __forceinline__ float rcp_cr(float x) {
+    if (__builtin_amdgcn_ballot_w64(!rt_cr_domain(__float_as_uint(x) & 0x7FFFFFFFu)) == 0) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        return fmaf(fmaf(-x, r, 1.0f), r, r);
+    }
+    return 1.0f / x;
+}
+#else
+RT_HD float sqrt_cr(float x) { return sqrtf(x); }
+RT_HD float rcp_cr(float x) { return 1.0f / x; }
+#endif
+RT_HD float length(f3 a) { return sqrt_cr(dot(a, a)); }
 // normalize(v) = v * (1 / sqrt(dot(v,v)))
-RT_HD f3 normalize(f3 a) { return a * (1.0f / sqrtf(dot(a, a))); }
+RT_HD f3 normalize(f3 a) { return a * rcp_cr(sqrt_cr(dot(a, a))); }
 RT_HD float saturate(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
 // Halton bases: `constant unsigned int primes[]` (RTrace/sampling.metal:97-104).

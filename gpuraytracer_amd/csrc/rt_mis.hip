@@ -61,14 +61,14 @@ __device__ __forceinline__ float smith_g1(float NoV, float roughness) {
     const float a = roughness * roughness;
     const float a2 = a * a;
     const float NoV2 = NoV * NoV;
-    return 2.0f / (1.0f + sqrtf(1.0f + (a2 * (1.0f - NoV2)) / NoV2));
+    return 2.0f / (1.0f + sqrt_cr(1.0f + (a2 * (1.0f - NoV2)) / NoV2));
 }
 
 // V_SmithGGXCorrelated (:203-208)
 __device__ __forceinline__ float v_smith(float NoV, float NoL, float a) {
     const float a2 = a * a;
-    const float GGXL = NoV * sqrtf(((-NoL) * a2 + NoL) * NoL + a2);
-    const float GGXV = NoL * sqrtf(((-NoV) * a2 + NoV) * NoV + a2);
+    const float GGXL = NoV * sqrt_cr(((-NoL) * a2 + NoL) * NoL + a2);
+    const float GGXV = NoL * sqrt_cr(((-NoV) * a2 + NoV) * NoV + a2);
     return 0.5f / (GGXV + GGXL);
 }
 
@@ -130,8 +130,8 @@ __device__ __forceinline__ float power_h(float p1, float p2, float p3, float n) 
 // cosineWeightedRay direction (:355-374)
 __device__ __forceinline__ f3 cosine_dir(f3 n, f3 t, f3 b, float ux, float uy) {
     const float phi = kTwoPiF * ux;
-    const float cosT = sqrtf(uy);
-    const float sinT = sqrtf(1.0f - uy);
+    const float cosT = sqrt_cr(uy);
+    const float sinT = sqrt_cr(1.0f - uy);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
     return normalize((t * (cp * sinT) + b * (sp * sinT)) + n * cosT);
@@ -145,9 +145,9 @@ __device__ __forceinline__ f3 vndf_dir(f3 V, f3 n, f3 t, f3 b, float roughness, 
     const f3 T2 = cross(Ve, T1);
     const float phi = kTwoPiF * ux;
     const float lenVe = length(Ve);
-    const float ctm = lenVe / sqrtf(1.0f + lenVe * lenVe);
+    const float ctm = lenVe / sqrt_cr(1.0f + lenVe * lenVe);
     const float ct = ctm + (1.0f - ctm) * uy;
-    const float st = sqrtf(1.0f - ct * ct);
+    const float st = sqrt_cr(1.0f - ct * ct);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
     const f3 h = normalize((T1 * (cp * st) + T2 * (sp * st)) + Ve * ct);

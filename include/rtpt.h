@@ -277,6 +277,12 @@ typedef struct rt_build_stats {
 } rt_build_stats;
 int rt_build_info(const rt_ctx* ctx, rt_build_stats* info);
 
+/* Self-check of the kernels' short correctly rounded sqrt and reciprocal
+ *  against the IEEE expansions on every one of the 2^32 float
+ * bit patterns, on the current device: mismatches[0] sqrt, [1] reciprocal
+ * (both 0 for a library whose results equal the oracle's). */
+int rt_math_selfcheck(uint64_t* mismatches);
+
 /* Hash of the sources this library was built from (gpuraytracer_amd/srchash.py:
  * csrc/ + include/): a loader can refuse a stale binary. */
 const char* rt_build_sha(void);

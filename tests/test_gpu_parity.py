@@ -571,3 +571,15 @@ def test_launch_lds_equals_staged_bytes_per_layout(case):
         info = r.last_launch()
     assert info["lds_bytes"] == lds, (info, layout)
     assert_parity(out, oracle_lib.render(s, sd, 2, 3), f"layout {layout}")
+
+
+def test_short_sqrt_and_reciprocal_equal_ieee_on_every_float():
+    """The kernels' sqrt_cr / rcp_cr (rt_math.h: a hardware rsq / rcp plus a
+    refinement, taken when every lane's argument is in [2^-100, 2^100)) equal the
+    IEEE sqrtf and 1/x -- the oracle's arithmetic -- on all 2^32 float bit
+    patterns (NaN results compare as NaN)."""
+    import ctypes
+    from gpuraytracer_amd import lib
+    bad = (ctypes.c_uint64 * 2)()
+    assert lib.rt_math_selfcheck(bad) == 0
+    assert list(bad) == [0, 0], list(bad)
