@@ -270,6 +270,12 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.W = cam.W;
     K.H = cam.H;
     memcpy(K.light_center, c->scene.light.center, sizeof(K.light_center));
+    {  // rt_kernel.hip shade(): the sample point's zero terms drop out exactly unless -0 is involved
+        uint32_t by, bz;
+        memcpy(&by, &K.light_center[1], 4);
+        memcpy(&bz, &K.light_center[2], 4);
+        K.light_plain = (by != 0x80000000u && bz != 0x80000000u) ? 1u : 0u;
+    }
     memcpy(K.light_color, c->scene.light.color, sizeof(K.light_color));
     K.spp = p->spp;
     K.sample_base = p->sample_base;

@@ -73,6 +73,10 @@ namespace {
 #ifndef RT_CENSUS
 #define RT_CENSUS 0
 #endif
+// RT_LQ: the light sample point and its cosine without their zero terms (shade)
+#ifndef RT_LQ
+#define RT_LQ 1
+#endif
 template <typename T>
 __device__ __forceinline__ T cz(T v) {
     asm volatile("" : "+v"(v));
@@ -173,13 +177,25 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     }
 #endif
     const f3 lcen = ld_f3(P.light_center);
-    const f3 q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
+    // q = center + (0.25,0,0)*ux + (0,0,0.25)*uy (sampling.metal:208-213).  The
+    // zero terms (0*ux, 0*uy: +-0, ux and uy are finite and never -0) drop out
+    // exactly: lcen.x + 0.25ux is never -0, so adding +-0 keeps it, and
+    // lcen.y (lcen.z) + +-0 is lcen.y (lcen.z) unless that is -0 -- the
+    // host's light_plain flag; otherwise the literal form
+    f3 q;
+    if (RT_LQ && P.light_plain)
+        q = f3{lcen.x + 0.25f * ux, lcen.y, lcen.z + 0.25f * uy};
+    else
+        q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
     f3 L = q - p;
     const float dist = length(L);
     const float inv = rcp_cr(fmaxf(dist, 1e-3f));
     L = L * inv;
     f3 lc = ld_f3(P.light_color) * (inv * inv);
-    lc = lc * saturate(dot(-L, f3{0.0f, -1.0f, 0.0f}));
+    // dot(-L, (0,-1,0)) = fma(-L.z, 0, fma(-L.y, -1, -L.x * 0)) is L.y exactly
+    // when L.y != 0; when L.y is +-0 either form gives a zero, which makes the
+    // light term zero (no shadow query, +0 added: the same result)
+    lc = lc * saturate(RT_LQ ? L.y : dot(-L, f3{0.0f, -1.0f, 0.0f}));
     lc = lc * saturate(dot(N, L));                         // :75
     s.thr = s.thr * diffuse;                               // :76
     // the light term lc * throughput (:87-89) and the next direction (:93-100)

@@ -71,6 +71,7 @@ struct KParams {
     uint32_t walk;            // rt_walk_scheduler: 0 auto, 1 lockstep, 2 free-running lanes, 3 sorted
     uint32_t wave_w;          // pixels per wave row (set by the launcher)
     uint32_t walk_leaf_den;   // free-running walks: leaf-round threshold, 0 = default
+    uint32_t light_plain;     // light_center.y, .z are not -0 (shade(): q without its zero terms)
     const float4* clusters;   // box clusters, kCluF4 float4 each, or null
     uint32_t nC;              // clusters (0: none)
     uint32_t pair_free;       // pairs in no cluster (bit mask)

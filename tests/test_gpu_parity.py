@@ -583,3 +583,18 @@ def test_short_sqrt_and_reciprocal_equal_ieee_on_every_float():
     bad = (ctypes.c_uint64 * 2)()
     assert lib.rt_math_selfcheck(bad) == 0
     assert list(bad) == [0, 0], list(bad)
+
+
+@pytest.mark.parametrize("comp", ["x", "y", "z"])
+def test_light_center_signed_zero(comp):
+    """shade() drops the zero terms of the light sample point (0*ux, 0*uy)
+    unless the light centre has a -0 y or z (the host's light_plain flag): a
+    centre component of -0 (the literal form for y, z; the short form for x)
+    and of +0 stay bit-exact vs the oracle."""
+    s = Scene.cornell_box(40, 24)
+    for val in (-0.0, 0.0):
+        setattr(s.light.center, comp, val)
+        sd = seed_splitmix(40, 24, key=3)
+        with Renderer(s, seeds=sd) as r:
+            out = r.render(RenderParams(spp=4, bounces=3))
+        assert_parity(out, oracle_lib.render(s, sd, 4, 3), f"light centre {comp}={val}")
