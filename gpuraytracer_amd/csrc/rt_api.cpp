@@ -576,7 +576,7 @@ int render_mis_impl(rt_ctx* c, const rt_mis_params* p, float* out, uint8_t* out8
     if (pb) {
         if ((st = ensure_staging(c, &c->d_mis_part, &c->mis_part_cap, pb, "hipMalloc(mis records)")) != RT_OK)
             return st;
-        K.part = reinterpret_cast<float*>(c->d_mis_part);
+        K.part = reinterpret_cast<float4*>(c->d_mis_part);
     }
 
     hipError_t e;

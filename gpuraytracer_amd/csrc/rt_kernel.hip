@@ -188,8 +188,11 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
     else
         q = (lcen + f3{0.25f, 0.0f, 0.0f} * ux) + f3{0.0f, 0.0f, 0.25f} * uy;
     f3 L = q - p;
-    const float dist = length(L);
-    const float inv = rcp_cr(fmaxf(dist, 1e-3f));
+    // the short correctly rounded forms (rt_math.h) except in the triangle-BVH
+    // kernel, where their uniform branches cost spills (scratch 16 -> 36 B)
+    constexpr bool CR = GEO != kGeoTriBvh;
+    const float dist = CR ? length(L) : length_ieee(L);
+    const float inv = CR ? rcp_cr(fmaxf(dist, 1e-3f)) : 1.0f / fmaxf(dist, 1e-3f);
     L = L * inv;
     f3 lc = ld_f3(P.light_color) * (inv * inv);
     // dot(-L, (0,-1,0)) = fma(-L.z, 0, fma(-L.y, -1, -L.x * 0)) is L.y exactly
@@ -210,8 +213,8 @@ __device__ __forceinline__ bool shade(const KParams& P, const SceneView& sv, Pat
         const float cv = halton_dim<5 + 5 * b, SMALL, GEO == kGeoPairClu>(s.i, sv.htab);
         float sp, cp;
         sincos_pt(6.28318548f * cu, &sp, &cp);             // sampling.metal:40-48
-        const float ct = sqrt_cr(cv);
-        const float st = sqrt_cr(1.0f - ct * ct);
+        const float ct = CR ? sqrt_cr(cv) : sqrtf(cv);
+        const float st = CR ? sqrt_cr(1.0f - ct * ct) : sqrtf(1.0f - ct * ct);
         d2 = (right * (st * cp) + N * ct) + fwd * (st * sp);  // sampling.metal:65
     }
     if (FUSE && b + 1 < B) {
@@ -766,7 +769,7 @@ void path_trace_kernel(KParams P) {
             const float sx = ((fx + jx) / fW) * 2.0f - 1.0f;
             const float ty = -(((fy + jy) / fH) * 2.0f - 1.0f);
             const float sh = sx * P.halfW, th = ty * P.halfH;
-            s.d = normalize((cu * sh + cv * th) - cw);
+            s.d = GEO != kGeoTriBvh ? normalize((cu * sh + cv * th) - cw) : normalize_ieee((cu * sh + cv * th) - cw);
             s.o = ld_f3(P.cam_pos);
             s.thr = f3{1.0f, 1.0f, 1.0f};
 #if RT_CENSUS == 1

@@ -159,7 +159,7 @@ struct MisParams {
     float l_width, l_depth, l_area, exposure;
     uint32_t camera_rays, S;   // S = misSamples / 3 (samples per strategy)
     uint32_t row_start, row_step, row_count;
-    float* part;               // split launches: 3 float planes per record and pixel, or null (rt_mis.hip SPLIT)
+    float4* part;              // split launches: one float4 per record and pixel, or null (rt_mis.hip SPLIT)
 };
 hipError_t launch_mis(const MisParams& P, SceneMem mem, hipStream_t stream);
 size_t mis_lds_bytes(uint32_t n_tri, uint32_t n_pairs);

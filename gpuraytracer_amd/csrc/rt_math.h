@@ -85,6 +85,11 @@ RT_HD float rcp_cr(float x) { return 1.0f / x; }
 RT_HD float length(f3 a) { return sqrt_cr(dot(a, a)); }
 // normalize(v) = v * (1 / sqrt(dot(v,v)))
 RT_HD f3 normalize(f3 a) { return a * rcp_cr(sqrt_cr(dot(a, a))); }
+// The same values through the IEEE expansions: for kernels where the short
+// forms' uniform branch costs registers (the triangle-BVH kernel spilled 20
+// more bytes per lane with them)
+RT_HD float length_ieee(f3 a) { return sqrtf(dot(a, a)); }
+RT_HD f3 normalize_ieee(f3 a) { return a * (1.0f / sqrtf(dot(a, a))); }
 RT_HD float saturate(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
 // Halton bases: `constant unsigned int primes[]` (RTrace/sampling.metal:97-104).

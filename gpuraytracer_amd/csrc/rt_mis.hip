@@ -61,14 +61,14 @@ __device__ __forceinline__ float smith_g1(float NoV, float roughness) {
     const float a = roughness * roughness;
     const float a2 = a * a;
     const float NoV2 = NoV * NoV;
-    return 2.0f / (1.0f + sqrt_cr(1.0f + (a2 * (1.0f - NoV2)) / NoV2));
+    return 2.0f / (1.0f + sqrtf(1.0f + (a2 * (1.0f - NoV2)) / NoV2));
 }
 
 // V_SmithGGXCorrelated (:203-208)
 __device__ __forceinline__ float v_smith(float NoV, float NoL, float a) {
     const float a2 = a * a;
-    const float GGXL = NoV * sqrt_cr(((-NoL) * a2 + NoL) * NoL + a2);
-    const float GGXV = NoL * sqrt_cr(((-NoV) * a2 + NoV) * NoV + a2);
+    const float GGXL = NoV * sqrtf(((-NoL) * a2 + NoL) * NoL + a2);
+    const float GGXV = NoL * sqrtf(((-NoV) * a2 + NoV) * NoV + a2);
     return 0.5f / (GGXV + GGXL);
 }
 
@@ -130,8 +130,8 @@ __device__ __forceinline__ float power_h(float p1, float p2, float p3, float n) 
 // cosineWeightedRay direction (:355-374)
 __device__ __forceinline__ f3 cosine_dir(f3 n, f3 t, f3 b, float ux, float uy) {
     const float phi = kTwoPiF * ux;
-    const float cosT = sqrt_cr(uy);
-    const float sinT = sqrt_cr(1.0f - uy);
+    const float cosT = sqrtf(uy);
+    const float sinT = sqrtf(1.0f - uy);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
     return normalize((t * (cp * sinT) + b * (sp * sinT)) + n * cosT);
@@ -145,9 +145,9 @@ __device__ __forceinline__ f3 vndf_dir(f3 V, f3 n, f3 t, f3 b, float roughness, 
     const f3 T2 = cross(Ve, T1);
     const float phi = kTwoPiF * ux;
     const float lenVe = length(Ve);
-    const float ctm = lenVe / sqrt_cr(1.0f + lenVe * lenVe);
+    const float ctm = lenVe / sqrtf(1.0f + lenVe * lenVe);
     const float ct = ctm + (1.0f - ctm) * uy;
-    const float st = sqrt_cr(1.0f - ct * ct);
+    const float st = sqrtf(1.0f - ct * ct);
     float sp, cp;
     sincos_pt(phi, &sp, &cp);
     const f3 h = normalize((T1 * (cp * st) + T2 * (sp * st)) + Ve * ct);
@@ -409,7 +409,7 @@ __device__ __forceinline__ void mis_store(const MisParams& P, size_t o, f3 acc) 
 }
 
 // SPLIT: one workgroup per (tile, round) -- blockIdx.z is the round -- and every
-// lane stores its camera ray's result (c, has) to P.part[i][pixel]; mis_sum_kernel
+// lane stores its camera ray's result to the records buffer (mis_part_bytes); mis_sum_kernel
 // then adds a pixel's rays in order i.  Twice the workgroups of half the length:
 // the frame's last workgroups (the tail, when too few are left to fill the GPU)
 // end sooner.
@@ -560,19 +560,12 @@ __global__ __launch_bounds__(kBlockThreads, kMisWavesPerEu) void mis_kernel(MisP
                     const f3 ck{__shfl(c.x, base + (int)k), __shfl(c.y, base + (int)k), __shfl(c.z, base + (int)k)};
                     if (__shfl((int)has, base + (int)k) != 0) acc = acc + ck;
                 }
-                if ((t3 & 63u) % ML == 0) {
-                    P.part[px] = acc.x;
-                    P.part[npix + px] = acc.y;
-                    P.part[2 * npix + px] = acc.z;
-                }
+                if ((t3 & 63u) % ML == 0) P.part[px] = make_float4(acc.x, acc.y, acc.z, 0.0f);
             } else if (i < P.camera_rays) {
                 // record i - ML + 1: this ray's c, which is +0 without a hit --
                 // adding it equals skipping it (the sum starts at +0, so it is
                 // never -0, and x + (+0) == x for every other x, NaN included)
-                float* rec = P.part + (size_t)3 * (i - ML + 1u) * npix + px;
-                rec[0] = c.x;
-                rec[npix] = c.y;
-                rec[2 * npix] = c.z;
+                P.part[(size_t)(i - ML + 1u) * npix + px] = make_float4(c.x, c.y, c.z, 0.0f);
             }
             continue;
         }
@@ -611,20 +604,23 @@ __global__ void mis_sum_kernel(MisParams P) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
     if (x >= (uint32_t)P.W) return;
     const size_t npix = (size_t)P.row_count * (size_t)P.W, o = (size_t)j * (size_t)P.W + x;
-    f3 acc{P.part[o], P.part[npix + o], P.part[2 * npix + o]};  // rays 0 .. ML-1
+    const float4 r0 = P.part[o];
+    f3 acc{r0.x, r0.y, r0.z};  // rays 0 .. ML-1
     for (uint32_t i = kMisLanes; i < P.camera_rays; ++i) {
-        const float* rec = P.part + (size_t)3 * (i - kMisLanes + 1u) * npix + o;
-        acc = acc + f3{rec[0], rec[npix], rec[2 * npix]};
+        const float4 v = P.part[(size_t)(i - kMisLanes + 1u) * npix + o];
+        acc = acc + f3{v.x, v.y, v.z};
     }
     mis_store(P, o, acc);
 }
 
 constexpr size_t kMisStashBytes = 15u * kBlockThreads * sizeof(float);  // per lane: primary hit, pixel sum, dl/dc, strategy sum
 
-// SPLIT launches (RT_MIS_SPLIT): the records buffer, 12 B per record and pixel
-// (3 float planes per record): record 0 = round 0's rays already summed, then
-// one record per later ray -- camera_rays - ML + 1 records (round 5: 16 B per
-// ray with a hit flag, 46 MB at 800x600 x 6 rays; now 28.8 MB); 0 (no split)
+// SPLIT launches (RT_MIS_SPLIT): the records buffer, one float4 per record and
+// pixel: record 0 = round 0's rays already summed, then one record per later
+// ray -- camera_rays - ML + 1 records (round 5: one per ray, 46 MB at 800x600 x
+// 6 rays; now 38.4 MB).  16 B, not 12: a wave's 8-pixel tile rows then write
+// whole 128-B lines (three 12-B float planes wrote 32-B row pieces: 51.6 MB of
+// HBM writes for 28.8 MB of records, profiles/r6/ab_results.md); 0 (no split)
 // when it would exceed kMisPartMax or the split is off.
 #ifndef RT_MIS_SPLIT
 #define RT_MIS_SPLIT 1
@@ -632,7 +628,7 @@ constexpr size_t kMisStashBytes = 15u * kBlockThreads * sizeof(float);  // per l
 constexpr size_t kMisPartMax = (size_t)256 << 20;
 size_t mis_part_bytes(uint32_t camera_rays, size_t pixels) {
     if (camera_rays <= kMisLanes) return 0u;
-    const size_t b = (size_t)(camera_rays - kMisLanes + 1u) * pixels * 3u * sizeof(float);
+    const size_t b = (size_t)(camera_rays - kMisLanes + 1u) * pixels * sizeof(float4);
     return (RT_MIS_SPLIT && camera_rays > kMisLanes && b <= kMisPartMax) ? b : 0u;
 }
 
