@@ -1028,7 +1028,10 @@ inline int lanes_per_pixel(const KParams& P, int geo) {
     // of N = 8 19,450 vs 18,824); whole frames of >= 1 M pixels keep 4 (1080p
     // 20,288 vs 20,143; 4096^2 18,505 vs 17,978)
     const bool share16 = P.row_step > 1 && P.spp >= 16u * kHaltonTabMinRounds;
-    const int want = (px >= 1000000ull && geo != kGeoSphLds && !share16) ? 4 : 16;
+    // the BVH walk kernels (spheres, and since round 6 triangles) take 16 at any
+    // size: triangles 100k / 10k / 1M at 1080p x 64 spp 1,176 / 1,234 / 575
+    // Msamples/s with 16 lanes vs 1,101 / 1,172 / 514 with 4
+    const int want = (px >= 1000000ull && geo != kGeoSphLds && geo != kGeoTriBvh && !share16) ? 4 : 16;
     if (P.spp >= (uint32_t)want) return want;
     return P.spp >= 4 ? 4 : 1;
 }
