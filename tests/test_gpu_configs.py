@@ -183,7 +183,7 @@ C4_GRID = (1920 // 2, 1080 // 2)
 def test_c4_timed_launch_1080p_256spp_bands_vs_oracle():
     """Config 4 exactly as the bench times it: the whole 1920x1080 frame of the
     1000-sphere scene at 256 spp in ONE launch (16 lanes per pixel, 16 rounds
-    per lane, C4_BLOCK-thread workgroups walking the compact 8-layout BVH in
+    per lane, C4_BLOCK-thread workgroups walking the 8-layout leaf-box BVH in
     L2, grid C4_GRID).  Three 4-row bands of that frame (top, middle, lower
     third) are compared with the brute-force oracle bit for bit (5.9 M
     samples on the host); the whole frame is finite with alpha 1."""
@@ -201,3 +201,21 @@ def test_c4_timed_launch_1080p_256spp_bands_vs_oracle():
     for start in (100, 540, 900):
         ref = oracle_lib.render(s, sd, 256, 3, row_start=start, row_count=4, threads=16)
         assert_parity(frame[start:start + 4], ref, f"C4 rows {start}+4 x 256 spp")
+
+
+def test_triangle_bvh_whole_1080p_frame_rows_vs_oracle():
+    """The triangle-BVH kernel as the triangle benches run it: a whole 1920x1080
+    frame of the room + 10k random triangles (GPU SAH build, 16 lanes per pixel,
+    select-form steps checked every 4) at 16 spp in one launch; a row of the
+    middle and one of the lower third against the brute-force oracle bit for bit."""
+    W, H = 1920, 1080
+    s = Scene.random_triangles(W, H, 10_000)
+    sd = seed_splitmix(W, H)
+    with Renderer(s, seeds=sd) as r:
+        frame = r.render(RenderParams(spp=16, bounces=3))
+        info = r.last_launch()
+    assert info["kernel"] == "rt::path_trace_kernel<3, 5, false, true, 16>", info
+    assert np.isfinite(frame).all() and np.all(frame[..., 3] == 1.0)
+    for start, n in ((540, 1), (800, 1)):
+        ref = oracle_lib.render(s, sd, 16, 3, row_start=start, row_count=n, threads=16)
+        assert_parity(frame[start:start + n], ref, f"10k triangles rows {start}+{n}")
