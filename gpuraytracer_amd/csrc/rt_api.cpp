@@ -36,6 +36,7 @@ struct rt_ctx {
     float4* d_tri_shade = nullptr;
     float4* d_pair_isect = nullptr;
     float4* d_clusters = nullptr;
+    float4* d_clu_oct = nullptr;     // rt_scene.hpp clu_oct
     uint32_t* d_sph_lds = nullptr;
     uint16_t* d_sph_lds_id = nullptr;
     uint4* d_sph_box = nullptr;      // the leaf-box layout of the sphere BVH (rt_scene.hpp sph_box)
@@ -136,6 +137,7 @@ void release(rt_ctx* c) {
     (void)hipFree(c->d_tri_shade);
     (void)hipFree(c->d_pair_isect);
     (void)hipFree(c->d_clusters);
+    (void)hipFree(c->d_clu_oct);
     (void)hipFree(c->d_sph_lds);
     (void)hipFree(c->d_sph_lds_id);
     (void)hipFree(c->d_sph_box);
@@ -239,6 +241,7 @@ int render_impl(rt_ctx* c, const rt_render_params* p, void* out, bool out_is_dev
     K.tri_shade = c->d_tri_shade;
     K.pair_isect = c->d_pair_isect;
     K.clusters = c->d_clusters;
+    K.clu_oct = c->d_clu_oct;
     K.nC = (uint32_t)(c->scene.clusters.size() / (4 * rt::kCluF4));
     K.pair_free = c->scene.pair_free_mask;
     K.sph_isect = c->d_sph_isect;
@@ -731,6 +734,7 @@ int rt_create_ex(const rt_scene_desc* d, const rt_create_options* opt, rt_ctx** 
             (e = upload(&c->d_tri_shade, s.tri_shade.data(), s.tri_shade.size() * sizeof(rt::TriShade), c->stream)) != hipSuccess ||
             (e = upload(&c->d_pair_isect, s.pair_isect.data(), s.pair_isect.size() * sizeof(rt::PairIsect), c->stream)) != hipSuccess ||
             (e = upload(&c->d_clusters, s.clusters.data(), s.clusters.size() * sizeof(float), c->stream)) != hipSuccess ||
+            (e = upload(&c->d_clu_oct, s.clu_oct.data(), s.clu_oct.size() * sizeof(float), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_lds, s.sph_lds.data(), s.sph_lds.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_lds_id, s.sph_lds_id.data(), s.sph_lds_id.size() * sizeof(uint16_t), c->stream)) != hipSuccess ||
             (e = upload(&c->d_sph_box, s.sph_box.data(), s.sph_box.size() * sizeof(uint32_t), c->stream)) != hipSuccess ||

@@ -633,7 +633,7 @@ void path_trace_kernel(KParams P) {
         constexpr bool pairs = GEO == kGeoPairLds || GEO == kGeoPairClu || GEO == kGeoSphLds;
         const uint32_t ng4 = pairs ? kPairF4 * sv.nP : 3u * sv.nT;
         const float4* src = pairs ? P.pair_isect : P.tri_isect;
-        RT_LDS_GUARD(16 * (size_t)(ng4 + (GEO == kGeoPairClu ? kCluF4 * P.nC : 0u)) +
+        RT_LDS_GUARD(16 * (size_t)(ng4 + (GEO == kGeoPairClu ? (kCluF4 + kCluOctF4) * P.nC : 0u)) +
                      (GEO == kGeoPairClu ? 4 * (size_t)kHaltonTabFloats : 0));
         for (uint32_t k = threadIdx.x; k < ng4; k += NT) lds[k] = src[k];
         if (GEO == kGeoSphLds) {  // the compact sphere BVH (8 layouts) stays in global memory (L2)
@@ -646,11 +646,13 @@ void path_trace_kernel(KParams P) {
         }
         if (GEO == kGeoPairClu) {  // box clusters after the pair records, then the Halton tables
             for (uint32_t k = threadIdx.x; k < kCluF4 * P.nC; k += NT) lds[ng4 + k] = P.clusters[k];
+            for (uint32_t k = threadIdx.x; k < kCluOctF4 * P.nC; k += NT)
+                lds[ng4 + kCluF4 * P.nC + k] = P.clu_oct[k];
+            sv.clu_oct = kCluOctF4 ? lds + ng4 + kCluF4 * P.nC : nullptr;
+            const uint32_t tab0 = ng4 + (kCluF4 + kCluOctF4) * P.nC;
             const bool tab = halton_tables_on(GEO, SMALL, P.spp, L);
-            sv.htab = tab ? reinterpret_cast<const float*>(lds + ng4 + kCluF4 * P.nC) : nullptr;
-            if (tab)
-                fill_halton_tables(reinterpret_cast<float*>(lds + ng4 + kCluF4 * P.nC), threadIdx.x,
-                                   NT);
+            sv.htab = tab ? reinterpret_cast<const float*>(lds + tab0) : nullptr;
+            if (tab) fill_halton_tables(reinterpret_cast<float*>(lds + tab0), threadIdx.x, NT);
         }
         __syncthreads();
         sv.tri = lds;

@@ -29,6 +29,12 @@ constexpr uint32_t kPairF4 = 7;  // float4 per pair record: 5 geometry + 2 padde
 constexpr uint32_t kSphBlockThreads = 64;
 constexpr size_t kSphPairLdsMaxBytes = 6 * 1024;
 constexpr uint32_t kCluF4 = 7;   // float4 per box cluster (rt_scene.hpp CompiledScene::clusters)
+// The path-trace kernel's cluster test reads the face masks of world axes from
+// a per-octant table, pre-swapped on the host (rt_trace.hpp cluster_candidates)
+#ifndef RT_CLU_OCT
+#define RT_CLU_OCT 0
+#endif
+constexpr uint32_t kCluOctF4 = RT_CLU_OCT ? 16u : 0u;  // float4 per box cluster of the octant mask table (CompiledScene::clu_oct)
 // Layouts of the triangle BVH (rt_scene.cpp build_tri_sah / rt_lbvh.hip,
 // rt_trace.hpp tri_cbvh_*): one per direction octant, 16 B per node.
 constexpr uint32_t kTriCompactLayouts = 8;
@@ -73,6 +79,7 @@ struct KParams {
     uint32_t walk_leaf_den;   // free-running walks: leaf-round threshold, 0 = default
     uint32_t light_plain;     // light_center.y, .z are not -0 (shade(): q without its zero terms)
     const float4* clusters;   // box clusters, kCluF4 float4 each, or null
+    const float4* clu_oct;    // per cluster and octant: pre-swapped face masks, kCluOctF4 float4 per cluster
     uint32_t nC;              // clusters (0: none)
     uint32_t pair_free;       // pairs in no cluster (bit mask)
 };
@@ -100,14 +107,16 @@ enum KernelLayout : int {
 constexpr uint32_t kHaltonTabLdsFloats = 4679;
 constexpr uint32_t kSortLdsF4 = 1097;
 // THE dynamic LDS of a workgroup of layout `lay`: the bytes its staging loops
-// write (pair / triangle records, then box clusters, then the Halton tables;
+// write (pair / triangle records, then box clusters and their octant mask
+// table, then the Halton tables;
 // the sorted kernels' path buffers first).  The launcher requests exactly this
 // and the kernels place their staged arrays by the same terms; an
 // -DRT_LDS_CHECK build also checks it against the dispatch's LDS allocation.
 __host__ __device__ constexpr size_t staged_lds_bytes(int lay, uint32_t nT, uint32_t nP, uint32_t nC) {
     return lay == kLayTriLds ? (size_t)48 * nT
            : (lay == kLayPairLds || lay == kLaySphLds || lay == kLayFreeSph) ? (size_t)16 * kPairF4 * nP
-           : lay == kLayPairClu ? (size_t)16 * (kPairF4 * nP + kCluF4 * nC) + (size_t)4 * kHaltonTabLdsFloats
+           : lay == kLayPairClu ? (size_t)16 * (kPairF4 * nP + (kCluF4 + kCluOctF4) * nC) +
+                                      (size_t)4 * kHaltonTabLdsFloats
            : (lay == kLayPairSorted || lay == kLaySortSph) ? (size_t)16 * (kSortLdsF4 + kPairF4 * nP)
            : lay == kLaySortTri ? (size_t)16 * kSortLdsF4
            : (size_t)0;  // TriGlobal, PairSmem, TriBvh, FreeTri: the scene stays in global memory

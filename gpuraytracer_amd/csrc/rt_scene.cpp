@@ -1081,6 +1081,21 @@ static void build_clusters(CompiledScene* out, const rt_float3* verts, uint32_t 
     multi.insert(multi.end(), single.begin(), single.end());
     out->clusters.swap(multi);
     out->pair_free_mask = free_mask;
+    out->clu_oct.clear();
+    for (size_t c = 0; c < out->clusters.size() / rec; ++c) {
+        const float* r = &out->clusters[c * rec];
+        uint32_t flags;
+        memcpy(&flags, &r[15], 4);
+        for (uint32_t oct = 0; oct < 8; ++oct) {
+            float m[6];
+            for (int s = 0; s < 6; ++s) m[s] = r[16 + s];
+            for (int a = 0; a < 3; ++a)
+                if ((flags >> a & 1u) && (oct >> a & 1u)) std::swap(m[2 * a], m[2 * a + 1]);
+            out->clu_oct.insert(out->clu_oct.end(), m, m + 6);
+            out->clu_oct.push_back(r[22]);  // all faces
+            out->clu_oct.push_back(0.0f);
+        }
+    }
 }
 
 static bool finite3(const rt_float3& v) {

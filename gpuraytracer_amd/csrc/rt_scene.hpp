@@ -118,6 +118,12 @@ struct CompiledScene {
     // = axis a is world axis a (+), bit 3 = container, bit 4 = single face;
     // w_a = face-plane half width factor of axis a.
     std::vector<float> clusters;
+    // Per cluster and ray-direction octant (8 floats, cluster-major): the face
+    // masks m0..m5 with the two faces of every world axis swapped when the
+    // octant's bit for that axis is set (the ray enters through the high face),
+    // then all, 0 -- the path-trace kernel's cluster test reads the entry /
+    // exit masks of world axes without a per-lane select (rt_trace.hpp).
+    std::vector<float> clu_oct;
     uint32_t pair_free_mask = 0;        // pairs in no cluster (tested by every lane)
     float tri_lo[3], tri_hi[3];         // bounds of the triangle vertices (BVH build)
     float margin = 0.0f;                // culling margin

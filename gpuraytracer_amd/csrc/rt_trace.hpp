@@ -154,7 +154,8 @@ struct SceneView {
     const uint32_t* tperm;    // leaf order -> triangle id
     uint32_t nTN;
     uint32_t nT, nP, nS, nN;
-    const float4* clu;        // box clusters, 4 float4 each (kGeoPairClu)
+    const float4* clu;        // box clusters, kCluF4 float4 each (kGeoPairClu)
+    const float4* clu_oct = nullptr;  // per cluster, 8 octants x 2 float4 of pre-swapped face masks, or null
     uint32_t nC;
     uint32_t pair_free;       // pairs in no cluster: tested by every lane
     const float* htab;        // Halton low-digit tables in LDS (kGeoPairClu)
@@ -841,10 +842,17 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
     const float oi[3] = {rb.oinv.x, rb.oinv.y, rb.oinv.z};
     uint32_t mask = 0;
     uint32_t c = 0;
+    // the face masks: the cluster record's, or with the octant table the row of
+    // this ray's octant, where world axes need no select (rt_scene.cpp clu_oct)
+    const bool oct = RT_CLU_OCT && sv.clu_oct != nullptr;  // wave-uniform
+    const uint32_t octant = (iv[0] < 0.0f ? 1u : 0u) | (iv[1] < 0.0f ? 2u : 0u) | (iv[2] < 0.0f ? 4u : 0u);
+    const float4* mrow = oct ? sv.clu_oct + 2u * octant : sv.clu + 4;
+    const uint32_t mstride = oct ? kCluOctF4 : kCluF4;
     for (; c < sv.nC; ++c) {
         if (SEG && ((skip >> c) & 1u)) continue;
         const float4* r = sv.clu + kCluF4 * c;
-        const float4 H = r[3], M0 = r[4], M1 = r[5], W = r[6];
+        const float4 H = r[3], W = r[6];
+        const float4 M0 = mrow[mstride * c], M1 = mrow[mstride * c + 1];
         const uint32_t flags = __float_as_uint(H.w);
         if (flags & 16u) break;  // single-face clusters come last (rt_scene.cpp)
         const float hi[3] = {H.x, H.y, H.z}, wf[3] = {W.x, W.y, W.z};
@@ -878,8 +886,12 @@ __device__ __forceinline__ uint32_t cluster_candidates(const SceneView& sv, f3 o
             // a ray with d_a >= 0 enters through the low face (slot 2a) and
             // leaves through the high one (2a + 1); the face plane lies
             // wf * |1/d_a| inside the padded slab, +- the tolerance
-            const bool neg = ida[a] < 0.0f;
-            const uint32_t m_en = neg ? m[2 * a + 1] : m[2 * a], m_ex = neg ? m[2 * a] : m[2 * a + 1];
+            uint32_t m_en = m[2 * a], m_ex = m[2 * a + 1];
+            if (!(RT_CLU_OCT && oct && (flags & (1u << a)))) {  // wave-uniform
+                const bool neg = ida[a] < 0.0f;
+                m_en = neg ? m[2 * a + 1] : m[2 * a];
+                m_ex = neg ? m[2 * a] : m[2 * a + 1];
+            }
             const float wa = wf[a] * fabsf(ida[a]);
             cm |= (en[a] + fmaf(fabsf(en[a]), kEps, wa) >= tlo) ? m_en : 0u;
             cm |= (ex[a] - fmaf(fabsf(ex[a]), kEps, wa) <= thi) ? m_ex : 0u;
